@@ -1,0 +1,285 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident Bloom-filter build throughput on MI355X.
+
+Workload (BASELINE.json configs[1]): one LSM run of
+16,777,216 int32 keys (generator --puts 16777216, seed 13141 + rank),
+m = (long)(16777216 * 10.0f) = 167,772,160 bits, k = 3 (the reference's
+three fixed hashes; config 2's "k=7" is not expressible bit-exactly).
+A step = clear the filter + build it from the device-resident key vector
+(bloomhip_set_batch).  With --gpus N every rank builds its own run on its own
+GPU (per-run sharding, no collective on the data path): weak scaling.
+
+Also reported at N=1: the C3 batched probe (16.7M GETs x 5 level filters),
+the end-to-end (host keys -> filter -> host bitmap) rate, and the CPU
+baseline (the oracle's C restatement, 1 thread) on the same keys.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import hashlib
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    # name: (keys per run, bits per entry)
+    "c2": (16_777_216, 10.0),
+    "c5": (67_108_864, 10.0),
+    "c4": (268_435_456, 12.0),
+}
+BUILD_SLOTS = ("k_build_atomic", "k_build_lds", "k_part_bin", "k_part_apply",
+               "part_counts(memset)")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(keys, m, reps=5):
+    """The oracle's C restatement (oracle/bloom_oracle.c, -O2, 1 thread) building
+    the same filter — the reference's set() loop is sequential."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from bloom_oracle import COracle
+    C = COracle()
+    C.build(m, keys[:1_000_000])  # warm-up
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        C.build(m, keys)
+        times.append(time.perf_counter() - t0)
+    t = statistics.median(times)
+    return {"value": round(keys.size / t / 1e9, 5), "unit": "Gkeys/s", "cores": 1,
+            "kind": "port",
+            "sample": f"full C2 run: {keys.size} keys, m={m}; oracle/bloom_oracle.c -O2, "
+                      f"1 thread, median of {reps} ({t:.3f} s each)"}
+
+
+def pmc_traffic(workload):
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def probe_c3(torch, bh, steps, warmup):
+    from bloomhip import workloads as W
+    gets, levels = W.c3()
+    filters = []
+    for lvl, keys, m in levels:
+        f = bh.BloomFilter(m)
+        f.set_batch(keys)
+        filters.append(f)
+    dgets = torch.from_numpy(gets).cuda()
+    nw = (gets.size + 63) // 64
+    dout = torch.empty((len(filters), nw), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream()
+    for _ in range(warmup):
+        bh.test_batch(filters, dgets, out=dout, stream=s)
+    torch.cuda.synchronize()
+    f0 = filters[0]
+    f0.profile(True)
+    f0.profile_reset()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        bh.test_batch(filters, dgets, out=dout, stream=s)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    prof = f0.profile_read()["k_probe"]
+    f0.profile(False)
+    kms = prof["ms"] / prof["launches"]
+    hits = dout.cpu().numpy().view("uint64")
+    import numpy as np
+    hit_counts = [int(np.unpackbits(hits[j].view(np.uint8)).sum()) for j in range(len(filters))]
+    algo = 4 * gets.size + sum((m + 63) // 64 * 8 for _, _, m in levels) + len(levels) * nw * 8
+    return {"gkeys_s": round(gets.size / (wall * 1e9), 3),
+            "kernel_ms": round(kms, 4), "wall_ms": round(wall * 1e3, 4),
+            "algorithmic_bytes": algo,
+            "achieved_GBps": round(algo / (kms * 1e-3) / 1e9, 1),
+            "frac": round(algo / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "hits_per_level": hit_counts}
+
+
+def e2e_build(torch, bh, keys_np, m, reps=5):
+    """Host keys (pinned) -> device -> filter -> host bitmap, wall clock."""
+    import numpy as np
+    pinned = torch.from_numpy(keys_np).pin_memory()
+    f = bh.BloomFilter(m)
+    host_words = np.empty(f.nwords, dtype=np.uint64)
+    times = []
+    for i in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dk = pinned.cuda(non_blocking=True)
+        s = torch.cuda.current_stream()
+        f.clear(stream=s)
+        f.set_batch(dk, stream=s)
+        bh.lib().bloomhip_download(f.handle, host_words.ctypes.data, host_words.size,
+                                   s.cuda_stream)
+        t = time.perf_counter() - t0
+        if i:
+            times.append(t)
+    t = statistics.median(times)
+    return {"gkeys_s": round(keys_np.size / t / 1e9, 3), "ms": round(t * 1e3, 3),
+            "note": "pinned host keys H2D + clear + build + bitmap D2H, wall clock"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--strategy", default="auto", choices=["auto", "atomic", "lds", "partition"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip probe/e2e legs")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+
+    import bloomhip as bh
+    from bloomhip import workloads as W
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    n, bpe = WORKLOADS[args.workload]
+    seed = W.SEED + rank
+    keys = bh.gen_puts(seed, n)
+    m = bh.m_bits(n, bpe)
+    dkeys = torch.from_numpy(keys).cuda()
+    f = bh.BloomFilter(m, device=local)
+    strat = {"auto": bh.BUILD_AUTO, "atomic": bh.BUILD_ATOMIC, "lds": bh.BUILD_LDS,
+             "partition": bh.BUILD_PARTITION}[args.strategy]
+    f.set_strategy(strat)
+    resolved = bh.STRATEGY_NAMES[f.resolve_strategy(n)]
+    s = torch.cuda.current_stream()
+
+    for _ in range(args.warmup):
+        f.clear(stream=s)
+        f.set_batch(dkeys, stream=s)
+    torch.cuda.synchronize()
+
+    # Validity: the bitmap the timed steps produce is the oracle-pinned one.
+    verified = None
+    pins_path = os.path.join(ROOT, "tests", "golden", "pins.json")
+    if os.path.exists(pins_path):
+        pins = json.load(open(pins_path))["oracle"]
+        want = None
+        if args.workload == "c2" and seed == W.SEED:
+            want = pins["c2"]["sha256"]
+        elif args.workload == "c5" and rank < len(pins["c5"]):
+            want = pins["c5"][rank]["sha256"]
+        elif args.workload == "c4" and seed == W.SEED:
+            want = pins["c4"]["sha256"]
+        if want is not None:
+            got = hashlib.sha256(f.words().tobytes()).hexdigest()
+            verified = got == want
+            if not verified:
+                log(f"rank {rank}: BITMAP MISMATCH vs oracle fixture")
+
+    f.profile(True)
+    f.profile_reset()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        f.clear(stream=s)
+        f.set_batch(dkeys, stream=s)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = f.profile_read()
+    f.profile(False)
+
+    if dist:
+        ok = torch.tensor([0 if verified is False else 1], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        all_ok = bool(ok.item())
+    else:
+        all_ok = verified is not False
+
+    extras = {}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_extras:
+        log("probe C3 ...")
+        extras["probe_c3"] = probe_c3(torch, bh, max(5, args.steps // 5), 2)
+        log("e2e ...")
+        extras["e2e_build"] = e2e_build(torch, bh, keys, m)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline ...")
+        cpu = cpu_baseline(keys, m)
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * n * args.steps / elapsed / 1e9
+    kernels = {k: {"launches": v["launches"], "avg_ms": round(v["ms"] / v["launches"], 5)}
+               for k, v in prof.items()}
+    build_ms = sum(v["ms"] / v["launches"] for k, v in prof.items() if k in BUILD_SLOTS)
+    dominant = max((k for k in prof if k in BUILD_SLOTS),
+                   key=lambda k: prof[k]["ms"] / prof[k]["launches"])
+    algo = 4 * n + (m + 63) // 64 * 8
+    achieved = algo / (build_ms * 1e-3) / 1e9
+    pmc = pmc_traffic(args.workload)
+    line = {
+        "metric": "Bloom build Gkeys/s device-resident (C2: 16M int32 keys/run, 10 bits/key, "
+                  "k=3); achieved HBM GB/s vs roofline",
+        "value": round(value, 4),
+        "unit": "Gkeys/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32 keys, u64 hash arithmetic",
+        "data": "synthetic: generator --puts stream (MT19937 seed 13141+rank), device-resident",
+        "config": {"workload": f"{args.workload}: one run per GPU, {n} keys, m={m} bits "
+                               f"({bpe} bits/key), k=3, build strategy {resolved}",
+                   "keys_per_run": n, "m_bits": m, "parallelism": f"per-run sharding x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": (pmc or {}).get("hbm_bytes_per_build"),
+                     "kernel": "+".join(k for k in prof if k in BUILD_SLOTS),
+                     "dominant": dominant,
+                     "algorithmic_bytes": algo,
+                     "note": "achieved = (4N + m/8) / summed avg device time of the build's "
+                             "kernels per step (HIP events on the launch stream)"},
+        "cpu_baseline": cpu,
+        "kernels": kernels,
+        "verified_vs_oracle": all_ok if verified is not None or dist else None,
+    }
+    line.update(extras)
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

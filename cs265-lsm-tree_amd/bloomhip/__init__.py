@@ -1,0 +1,327 @@
+"""bloomhip — Python view of the MI355X Bloom-filter engine's C ABI.
+
+Thin ctypes binding of ``include/bloomhip.h`` (``lib/libbloomhip.so``).  It
+mirrors the reference's filter surface (jackdent/cs265-lsm-tree
+src/bloom_filter.h:6-15) so tests read like the reference's own usage:
+
+    f = BloomFilter(m_bits)         # BloomFilter(long length)   bloom_filter.h:12
+    f.set(key)                      # void set(KEY_t)            bloom_filter.cpp:49-53
+    f.is_set(key)                   # bool is_set(KEY_t) const   bloom_filter.cpp:55-59
+
+plus the batch calls the GPU needs (``set_batch`` / ``test_batch``) and
+``m_bits(max_size, bits_per_entry)`` for Run::Run's sizing (src/run.cpp:13-15).
+
+There is no CPU fallback: if the HIP library is missing this module raises on
+import, and every compute call goes through the gfx950 kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(os.path.dirname(PKG_DIR), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libbloomhip.so")
+
+OK = 0
+EIO = -5
+ENOMEM = -12
+ENODEV = -19
+EINVAL = -22
+ERANGE = -34
+
+BUILD_AUTO = 0
+BUILD_ATOMIC = 1
+BUILD_LDS = 2
+BUILD_PARTITION = 3
+STRATEGY_NAMES = {BUILD_AUTO: "auto", BUILD_ATOMIC: "atomic", BUILD_LDS: "lds",
+                  BUILD_PARTITION: "partition"}
+PROF_SLOTS = 8
+
+# Every symbol include/bloomhip.h and include/bloomhip_workload.h declare.
+EXPORTED_SYMBOLS = (
+    "bloomhip_abi_version", "bloomhip_strerror", "bloomhip_last_error", "bloomhip_device_count",
+    "bloomhip_m_bits", "bloomhip_create", "bloomhip_destroy", "bloomhip_size",
+    "bloomhip_nwords", "bloomhip_device", "bloomhip_device_words", "bloomhip_stream",
+    "bloomhip_clear", "bloomhip_set_batch", "bloomhip_test_batch", "bloomhip_set",
+    "bloomhip_is_set", "bloomhip_download", "bloomhip_upload", "bloomhip_sync",
+    "bloomhip_set_strategy", "bloomhip_resolve_strategy", "bloomhip_profile_enable",
+    "bloomhip_profile_read", "bloomhip_profile_reset", "bloomhip_host_positions",
+    "bloomhip_gen_mt19937", "bloomhip_gen_glibc_rand", "bloomhip_gen_puts",
+    "bloomhip_gen_workload",
+)
+
+
+class BloomHipError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        lib = _lib()
+        msg = lib.bloomhip_strerror(status).decode()
+        detail = lib.bloomhip_last_error().decode()
+        super().__init__(f"{what}: {msg} ({status}){' — ' + detail if detail else ''}")
+        self.status = status
+
+
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"bloomhip: {LIB_PATH} is missing — build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        P, I, U64, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t
+        PU64 = ctypes.POINTER(ctypes.c_uint64)
+        sig = {
+            "bloomhip_abi_version": (I, []),
+            "bloomhip_strerror": (ctypes.c_char_p, [I]),
+            "bloomhip_last_error": (ctypes.c_char_p, []),
+            "bloomhip_device_count": (I, [ctypes.POINTER(I)]),
+            "bloomhip_m_bits": (I, [ctypes.c_int64, ctypes.c_float, PU64]),
+            "bloomhip_create": (I, [I, U64, ctypes.POINTER(P)]),
+            "bloomhip_destroy": (I, [P]),
+            "bloomhip_size": (I, [P, PU64]),
+            "bloomhip_nwords": (I, [P, PU64]),
+            "bloomhip_device": (I, [P, ctypes.POINTER(I)]),
+            "bloomhip_device_words": (I, [P, ctypes.POINTER(P)]),
+            "bloomhip_stream": (I, [P, ctypes.POINTER(P)]),
+            "bloomhip_clear": (I, [P, P]),
+            "bloomhip_set_batch": (I, [P, P, SZ, SZ, I, P]),
+            "bloomhip_test_batch": (I, [ctypes.POINTER(P), I, P, SZ, SZ, I, P, I, P]),
+            "bloomhip_set": (I, [P, ctypes.c_int32]),
+            "bloomhip_is_set": (I, [P, ctypes.c_int32, ctypes.POINTER(I)]),
+            "bloomhip_download": (I, [P, P, SZ, P]),
+            "bloomhip_upload": (I, [P, P, SZ, P]),
+            "bloomhip_sync": (I, [P, P]),
+            "bloomhip_set_strategy": (I, [P, I]),
+            "bloomhip_resolve_strategy": (I, [P, SZ, ctypes.POINTER(I)]),
+            "bloomhip_profile_enable": (I, [P, I]),
+            "bloomhip_profile_read": (I, [P, I, ctypes.POINTER(ctypes.c_char_p), PU64,
+                                          ctypes.POINTER(ctypes.c_double)]),
+            "bloomhip_profile_reset": (I, [P]),
+            "bloomhip_host_positions": (I, [U64, P, SZ, P]),
+            "bloomhip_gen_mt19937": (I, [ctypes.c_uint32, SZ, P]),
+            "bloomhip_gen_glibc_rand": (I, [ctypes.c_uint32, SZ, P]),
+            "bloomhip_gen_puts": (I, [ctypes.c_uint32, SZ, P, P]),
+            "bloomhip_gen_workload": (I, [ctypes.c_uint32, SZ, SZ, ctypes.c_float, ctypes.c_float,
+                                          P, P]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def lib():
+    return _lib()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != OK:
+        raise BloomHipError(rc, what)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = _lib().bloomhip_device_count(ctypes.byref(n))
+    return n.value if rc == OK else 0
+
+
+def m_bits(max_size: int, bits_per_entry: float) -> int:
+    """Run::Run's filter size (src/run.cpp:13-15): (long)((float)max_size * bpe)."""
+    out = ctypes.c_uint64()
+    _check(_lib().bloomhip_m_bits(int(max_size), float(bits_per_entry), ctypes.byref(out)),
+           "bloomhip_m_bits")
+    return out.value
+
+
+def host_positions(m: int, keys) -> np.ndarray:
+    """The engine's own position arithmetic evaluated on the host (self-test hook)."""
+    k = np.ascontiguousarray(keys, dtype=np.int32)
+    out = np.empty((k.size, 3), dtype=np.uint64)
+    _check(_lib().bloomhip_host_positions(m, k.ctypes.data, k.size, out.ctypes.data),
+           "bloomhip_host_positions")
+    return out
+
+
+def _ptr_of(buf):
+    """(address, on_device, keepalive) for a numpy array or a torch tensor."""
+    if isinstance(buf, np.ndarray):
+        if not buf.flags["C_CONTIGUOUS"]:
+            buf = np.ascontiguousarray(buf)
+        return buf.ctypes.data, 0, buf
+    # torch tensor (duck-typed so importing this module does not need torch)
+    if hasattr(buf, "data_ptr") and hasattr(buf, "is_cuda"):
+        if not buf.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return buf.data_ptr(), 1 if buf.is_cuda else 0, buf
+    arr = np.ascontiguousarray(buf, dtype=np.int32)
+    return arr.ctypes.data, 0, arr
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream  # torch.cuda.Stream
+
+
+class BloomFilter:
+    """One device-resident filter (a ``bloomhip_filter`` handle)."""
+
+    def __init__(self, m_bits: int, device: int = 0):
+        if m_bits <= 0:
+            raise BloomHipError(EINVAL, "BloomFilter(m_bits <= 0)")
+        h = ctypes.c_void_p()
+        _check(_lib().bloomhip_create(device, m_bits, ctypes.byref(h)), "bloomhip_create")
+        self._h = h
+        self.m = m_bits
+        self.device = device
+        n = ctypes.c_uint64()
+        _check(_lib().bloomhip_nwords(h, ctypes.byref(n)), "bloomhip_nwords")
+        self.nwords = n.value
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib().bloomhip_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # --- reference surface ------------------------------------------------
+    def set(self, key: int) -> None:
+        _check(_lib().bloomhip_set(self._h, int(key)), "bloomhip_set")
+
+    def is_set(self, key: int) -> bool:
+        hit = ctypes.c_int(0)
+        _check(_lib().bloomhip_is_set(self._h, int(key), ctypes.byref(hit)), "bloomhip_is_set")
+        return bool(hit.value)
+
+    # --- batches ----------------------------------------------------------
+    def set_batch(self, keys, n: int | None = None, stride: int = 4, stream=None) -> None:
+        ptr, on_dev, keep = _ptr_of(keys)
+        if n is None:
+            nbytes = keep.nbytes if isinstance(keep, np.ndarray) else keep.numel() * keep.element_size()
+            n = nbytes // stride
+        _check(_lib().bloomhip_set_batch(self._h, ptr, n, stride, on_dev, _stream_ptr(stream)),
+               "bloomhip_set_batch")
+
+    def clear(self, stream=None) -> None:
+        _check(_lib().bloomhip_clear(self._h, _stream_ptr(stream)), "bloomhip_clear")
+
+    def words(self) -> np.ndarray:
+        """Bitmap as ceil(m/64) uint64 blocks (dynamic_bitset layout)."""
+        out = np.empty(self.nwords, dtype=np.uint64)
+        _check(_lib().bloomhip_download(self._h, out.ctypes.data, out.size, None),
+               "bloomhip_download")
+        return out
+
+    def load_words(self, words: np.ndarray) -> None:
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        _check(_lib().bloomhip_upload(self._h, w.ctypes.data, w.size, None), "bloomhip_upload")
+
+    def device_words_ptr(self) -> int:
+        p = ctypes.c_void_p()
+        _check(_lib().bloomhip_device_words(self._h, ctypes.byref(p)), "bloomhip_device_words")
+        return p.value
+
+    def stream_ptr(self) -> int:
+        p = ctypes.c_void_p()
+        _check(_lib().bloomhip_stream(self._h, ctypes.byref(p)), "bloomhip_stream")
+        return p.value or 0
+
+    def sync(self, stream=None) -> None:
+        _check(_lib().bloomhip_sync(self._h, _stream_ptr(stream)), "bloomhip_sync")
+
+    def set_strategy(self, strategy: int) -> None:
+        _check(_lib().bloomhip_set_strategy(self._h, strategy), "bloomhip_set_strategy")
+
+    def resolve_strategy(self, n: int) -> int:
+        s = ctypes.c_int()
+        _check(_lib().bloomhip_resolve_strategy(self._h, n, ctypes.byref(s)),
+               "bloomhip_resolve_strategy")
+        return s.value
+
+    # --- profiling ----------------------------------------------------------
+    def profile(self, enable: bool = True) -> None:
+        _check(_lib().bloomhip_profile_enable(self._h, 1 if enable else 0), "profile_enable")
+
+    def profile_reset(self) -> None:
+        _check(_lib().bloomhip_profile_reset(self._h), "profile_reset")
+
+    def profile_read(self) -> dict:
+        res = {}
+        for slot in range(PROF_SLOTS):
+            name = ctypes.c_char_p()
+            launches = ctypes.c_uint64()
+            ms = ctypes.c_double()
+            _check(_lib().bloomhip_profile_read(self._h, slot, ctypes.byref(name),
+                                                ctypes.byref(launches), ctypes.byref(ms)),
+                   "profile_read")
+            if launches.value:
+                res[name.value.decode()] = {"launches": launches.value, "ms": ms.value}
+        return res
+
+
+def test_batch(filters: Sequence[BloomFilter], keys, n: int | None = None, stride: int = 4,
+               out=None, stream=None):
+    """is_set of every key against each filter.  Returns (or fills) a packed
+    [nf, ceil(n/64)] uint64 array: bit i%64 of row j word i/64 = filters[j].is_set(key i)."""
+    ptr, on_dev, keep = _ptr_of(keys)
+    if n is None:
+        nbytes = keep.nbytes if isinstance(keep, np.ndarray) else keep.numel() * keep.element_size()
+        n = nbytes // stride
+    nf = len(filters)
+    nw = (n + 63) // 64
+    if out is None:
+        out = np.zeros((nf, nw), dtype=np.uint64)
+    optr, out_dev, okeep = _ptr_of(out)
+    arr = (ctypes.c_void_p * nf)(*[f.handle.value for f in filters])
+    _check(_lib().bloomhip_test_batch(arr, nf, ptr, n, stride, on_dev, optr, out_dev,
+                                      _stream_ptr(stream)), "bloomhip_test_batch")
+    return out
+
+
+# --- workload streams (generator/generator.c restatement) --------------------
+def gen_mt19937(seed: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.uint32)
+    _check(_lib().bloomhip_gen_mt19937(seed, n, out.ctypes.data), "gen_mt19937")
+    return out
+
+
+def gen_glibc_rand(seed: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.int32)
+    _check(_lib().bloomhip_gen_glibc_rand(seed, n, out.ctypes.data), "gen_glibc_rand")
+    return out
+
+
+def gen_puts(seed: int, n: int, with_vals: bool = False):
+    keys = np.empty(n, dtype=np.int32)
+    vals = np.empty(n, dtype=np.int32) if with_vals else None
+    _check(_lib().bloomhip_gen_puts(seed, n, keys.ctypes.data,
+                                    vals.ctypes.data if with_vals else None), "gen_puts")
+    return (keys, vals) if with_vals else keys
+
+
+def gen_workload(seed: int, n_puts: int, n_gets: int, skew: float, miss_ratio: float):
+    puts = np.empty(n_puts, dtype=np.int32)
+    gets = np.empty(n_gets, dtype=np.int32)
+    _check(_lib().bloomhip_gen_workload(seed, n_puts, n_gets, skew, miss_ratio,
+                                        puts.ctypes.data, gets.ctypes.data), "gen_workload")
+    return puts, gets

@@ -1,0 +1,86 @@
+"""The benchmark configurations of BASELINE.json as concrete key vectors.
+
+Each config is restated from the reference's own call paths:
+
+C1  generator --puts 100000 (seed 13141), tree flags -b 100 -r 10: the buffer
+    holds 100*4096/8 = 51,200 entries (src/main.cpp:89); the first flush is a
+    run of the first 51,200 DISTINCT keys (Buffer::put, src/buffer.cpp:37-58),
+    written sorted as entry_t {key, val} (src/lsm_tree.cpp:124-129) — an AoS
+    run read at stride 8.  m = (long)(51200 * 10.0f) (src/run.cpp:15).
+C2  one run of 16,777,216 keys (generator --puts 16777216), 10 bits/key.
+C3  generator --puts 22347776 --gets 16777216 --gets-skewness 0.2
+    --gets-misses-ratio 0.3; tree -b 128 -d 5 -f 4 -r 10: level i holds one run
+    of capacity 65,536*4^i (src/lsm_tree.cpp:28-42); level 4 (oldest) is built
+    from puts[0, 16.78M), level 3 the next 4.19M, ... level 0 the newest
+    65,536.  Every GET probes all five filters.
+C4  one run of 268,435,456 keys, 12 bits/key.
+C5  runs r = 0..7 of 67,108,864 keys each (generator seed 13141 + r), 10 bits/key.
+
+k = 3 everywhere: the reference has three fixed hashes and no k parameter
+(src/bloom_filter.h:8-10), so config 2's "k=7" is not expressible bit-exactly.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import gen_puts, gen_workload, m_bits
+
+SEED = 13141
+
+C2_N = 16_777_216
+C2_BPE = 10.0
+C3_PUTS = 22_347_776
+C3_GETS = 16_777_216
+C3_LEVELS = 5
+C3_BASE_CAP = 65_536
+C3_FANOUT = 4
+C4_N = 268_435_456
+C4_BPE = 12.0
+C5_N = 67_108_864
+C5_RUNS = 8
+
+
+def c1_run(n_puts: int = 100_000, buffer_entries: int = 51_200, seed: int = SEED):
+    """(AoS entry_t run as int32[n, 2], m) for the first buffer flush."""
+    keys, vals = gen_puts(seed, n_puts, with_vals=True)
+    seen = {}
+    for k, v in zip(keys.tolist(), vals.tolist()):
+        if k in seen:
+            seen[k] = v          # Buffer::put updates an existing key
+            continue
+        if len(seen) == buffer_entries:
+            break                # buffer full: the flush happens here
+        seen[k] = v
+    items = sorted(seen.items())
+    run = np.array(items, dtype=np.int32).reshape(-1, 2)
+    return run, m_bits(buffer_entries, 10.0)
+
+
+def c2(seed: int = SEED, n: int = C2_N):
+    return gen_puts(seed, n), m_bits(n, C2_BPE)
+
+
+def c3_caps():
+    return [C3_BASE_CAP * C3_FANOUT ** i for i in range(C3_LEVELS)]
+
+
+def c3(seed: int = SEED):
+    """(gets, [(level, keys, m) for level 0..4]) — level 0 is the newest run."""
+    puts, gets = gen_workload(seed, C3_PUTS, C3_GETS, 0.2, 0.3)
+    caps = c3_caps()
+    levels = []
+    start = 0
+    for lvl in reversed(range(C3_LEVELS)):   # oldest (largest) run first in the stream
+        cap = caps[lvl]
+        levels.append((lvl, puts[start:start + cap], m_bits(cap, 10.0)))
+        start += cap
+    levels.sort(key=lambda t: t[0])
+    return gets, levels
+
+
+def c4(seed: int = SEED, n: int = C4_N):
+    return gen_puts(seed, n), m_bits(n, C4_BPE)
+
+
+def c5_run(r: int, n: int = C5_N):
+    return gen_puts(SEED + r, n), m_bits(n, 10.0)

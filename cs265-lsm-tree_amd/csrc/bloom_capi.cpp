@@ -1,0 +1,566 @@
+// bloom_capi.cpp — the C ABI of include/bloomhip.h: filter handles, stream
+// ordering, host staging, strategy selection and per-kernel timing around
+// the gfx950 kernels of bloom_kernels.hip.
+//
+// Reference surface replaced (jackdent/cs265-lsm-tree):
+//   BloomFilter(long)      src/bloom_filter.h:12      -> bloomhip_create
+//   set(KEY_t)             src/bloom_filter.cpp:49-53 -> bloomhip_set_batch / bloomhip_set
+//   is_set(KEY_t) const    src/bloom_filter.cpp:55-59 -> bloomhip_test_batch / bloomhip_is_set
+//   Run::Run sizing        src/run.cpp:13-15          -> bloomhip_m_bits
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/bloomhip.h"
+#include "bloom_kernels.h"
+
+using namespace bloomhip;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail_hip(hipError_t e, const char *what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+    if (e == hipErrorOutOfMemory) return BLOOMHIP_ENOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return BLOOMHIP_ENODEV;
+    return BLOOMHIP_EIO;
+}
+
+#define HIP_TRY(expr)                                       \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return fail_hip(_e, #expr);   \
+    } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+enum ProfSlot {
+    SLOT_CLEAR = 0,
+    SLOT_ATOMIC = 1,
+    SLOT_LDS = 2,
+    SLOT_PART_BIN = 3,
+    SLOT_PART_APPLY = 4,
+    SLOT_PROBE = 5,
+    SLOT_COUNTS = 6,
+    SLOT_COPY = 7,
+};
+const char *kSlotNames[BLOOMHIP_PROF_SLOTS] = {
+    "clear(memset)",          "k_build_atomic", "k_build_lds",      "k_part_bin",
+    "k_part_apply",           "k_probe",        "part_counts(memset)", "copy",
+};
+
+struct PendingTiming {
+    int slot;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct bloomhip_filter {
+    int device = 0;
+    uint64_t m = 0;
+    uint64_t nwords64 = 0;
+    uint32_t *d_words = nullptr;
+    hipStream_t stream = nullptr;
+    ModParams mp{};
+    int strategy = BLOOMHIP_BUILD_AUTO;
+    bool known_zero = true;  // host-side knowledge that every bit is 0
+
+    std::mutex mu;  // guards staging, workspace and profiling state
+    void *d_stage = nullptr;
+    size_t stage_bytes = 0;
+    void *d_out_stage = nullptr;
+    size_t out_stage_bytes = 0;
+    uint32_t *d_bins = nullptr;
+    size_t bins_bytes = 0;
+    uint32_t *d_counts = nullptr;
+
+    bool prof = false;
+    uint64_t prof_launches[BLOOMHIP_PROF_SLOTS] = {};
+    double prof_ms[BLOOMHIP_PROF_SLOTS] = {};
+    std::vector<PendingTiming> pending;
+    std::vector<hipEvent_t> spare_events;
+};
+
+namespace {
+
+hipStream_t pick_stream(const bloomhip_filter *f, void *stream) {
+    return stream ? reinterpret_cast<hipStream_t>(stream) : f->stream;
+}
+
+hipError_t grow(void **ptr, size_t *have, size_t need) {
+    if (*have >= need) return hipSuccess;
+    if (*ptr) {
+        hipError_t e = hipFree(*ptr);
+        if (e != hipSuccess) return e;
+        *ptr = nullptr;
+        *have = 0;
+    }
+    size_t sz = std::max<size_t>(need, 1 << 20);
+    hipError_t e = hipMalloc(ptr, sz);
+    if (e == hipSuccess) *have = sz;
+    return e;
+}
+
+hipEvent_t take_event(bloomhip_filter *f) {
+    if (!f->spare_events.empty()) {
+        hipEvent_t e = f->spare_events.back();
+        f->spare_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Runs `launch` on `s`, bracketed by events when profiling is enabled.
+template <class F>
+hipError_t timed(bloomhip_filter *f, int slot, hipStream_t s, F &&launch) {
+    if (!f->prof) return launch();
+    hipEvent_t a = take_event(f), b = take_event(f);
+    if (!a || !b) return launch();
+    (void)hipEventRecord(a, s);
+    hipError_t e = launch();
+    (void)hipEventRecord(b, s);
+    f->pending.push_back({slot, a, b});
+    return e;
+}
+
+int harvest_profile(bloomhip_filter *f) {
+    for (auto &p : f->pending) {
+        HIP_TRY(hipEventSynchronize(p.b));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
+        f->prof_ms[p.slot] += ms;
+        f->prof_launches[p.slot] += 1;
+        f->spare_events.push_back(p.a);
+        f->spare_events.push_back(p.b);
+    }
+    f->pending.clear();
+    return BLOOMHIP_OK;
+}
+
+int classify_keys(const void *keys, size_t stride, int *layout) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(keys);
+    if (stride < 4 || stride % 4 != 0 || (a & 3)) return BLOOMHIP_EINVAL;
+    if (stride == 4 && (a & 15) == 0) *layout = KEYS_PACKED;
+    else if (stride == 8 && (a & 15) == 0) *layout = KEYS_ENTRY;
+    else *layout = KEYS_STRIDED;
+    return BLOOMHIP_OK;
+}
+
+// Device-resident view of `n` keys: the caller's buffer, or a copy of a host
+// buffer into the handle's staging area (enqueued on s).
+int device_keys(bloomhip_filter *f, const void *keys, size_t n, size_t stride, int on_device,
+                hipStream_t s, KeySpan *out) {
+    int layout = 0;
+    if (n && !keys) return BLOOMHIP_EINVAL;
+    if (stride < 4 || stride % 4) return BLOOMHIP_EINVAL;
+    const void *dev = keys;
+    if (!on_device && n) {
+        const size_t bytes = (n - 1) * stride + 4;
+        HIP_TRY(grow(&f->d_stage, &f->stage_bytes, bytes));
+        int rc = timed(f, SLOT_COPY, s, [&] {
+            return hipMemcpyAsync(f->d_stage, keys, bytes, hipMemcpyHostToDevice, s);
+        });
+        if (rc != hipSuccess) return fail_hip((hipError_t)rc, "hipMemcpyAsync(keys H2D)");
+        dev = f->d_stage;
+    }
+    if (n) {
+        int rc = classify_keys(dev, stride, &layout);
+        if (rc) return rc;
+    }
+    *out = KeySpan{reinterpret_cast<const char *>(dev), n, stride, layout};
+    return BLOOMHIP_OK;
+}
+
+int resolve_strategy(const bloomhip_filter *f, size_t n) {
+    if (f->strategy != BLOOMHIP_BUILD_AUTO) return f->strategy;
+    if (!f->mp.fast) return BLOOMHIP_BUILD_ATOMIC;
+    const uint64_t bytes = (f->m + 7) / 8;
+    if (bytes <= kLdsBitmapBytes) {
+        // Worth a private LDS copy once the batch outweighs the merge.
+        return n >= (size_t)(f->m / 32) ? BLOOMHIP_BUILD_LDS : BLOOMHIP_BUILD_ATOMIC;
+    }
+    const uint64_t nbins = (f->m + (1ull << kSegBits) - 1) >> kSegBits;
+    if (nbins <= kPartMaxBins && n >= (size_t)nbins * 256) return BLOOMHIP_BUILD_PARTITION;
+    return BLOOMHIP_BUILD_ATOMIC;
+}
+
+int strategy_supported(const bloomhip_filter *f, int strategy) {
+    switch (strategy) {
+        case BLOOMHIP_BUILD_ATOMIC: return 1;
+        case BLOOMHIP_BUILD_LDS: return f->mp.fast && (f->m + 7) / 8 <= kLdsBitmapBytes;
+        case BLOOMHIP_BUILD_PARTITION:
+            return f->mp.fast && ((f->m + (1ull << kSegBits) - 1) >> kSegBits) <= kPartMaxBins;
+        default: return 0;
+    }
+}
+
+int run_partition(bloomhip_filter *f, const KeySpan &ks, hipStream_t s) {
+    const size_t nbins = (size_t)((f->m + (1ull << kSegBits) - 1) >> kSegBits);
+    // Expected positions per full segment, plus a wide margin: bins that
+    // still fill up spill into global atomics (exact, just slower).
+    const double expect = 3.0 * (double)ks.n * (double)(1ull << kSegBits) / (double)f->m;
+    size_t cap = (size_t)(expect + 8.0 * std::sqrt(expect) + 1024.0);
+    cap = std::min<size_t>((cap + 3) & ~(size_t)3, 3 * ks.n + 4);
+    cap = (cap + 3) & ~(size_t)3;
+    if (cap > 0xFFFFFFF0ull) return BLOOMHIP_ERANGE;
+    HIP_TRY(grow(reinterpret_cast<void **>(&f->d_bins), &f->bins_bytes, nbins * cap * 4));
+    if (!f->d_counts) HIP_TRY(hipMalloc(&f->d_counts, kPartMaxBins * 4));
+    PartitionWorkspace ws{f->d_bins, f->d_counts, cap, nbins};
+    hipError_t e = timed(f, SLOT_COUNTS, s, [&] {
+        return hipMemsetAsync(f->d_counts, 0, nbins * 4, s);
+    });
+    if (e != hipSuccess) return fail_hip(e, "hipMemsetAsync(counts)");
+    e = timed(f, SLOT_PART_BIN, s, [&] { return launch_part_bin(ks, f->mp, f->d_words, ws, s); });
+    if (e != hipSuccess) return fail_hip(e, "k_part_bin");
+    const int merge = f->known_zero ? 0 : 1;
+    e = timed(f, SLOT_PART_APPLY, s,
+              [&] { return launch_part_apply(f->mp, f->d_words, ws, merge, s); });
+    if (e != hipSuccess) return fail_hip(e, "k_part_apply");
+    return BLOOMHIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bloomhip_abi_version(void) { return BLOOMHIP_ABI_VERSION; }
+
+const char *bloomhip_strerror(int status) {
+    switch (status) {
+        case BLOOMHIP_OK: return "ok";
+        case BLOOMHIP_EIO: return "HIP runtime error";
+        case BLOOMHIP_ENOMEM: return "out of device memory";
+        case BLOOMHIP_ENODEV: return "no such device";
+        case BLOOMHIP_EINVAL: return "invalid argument";
+        case BLOOMHIP_ERANGE: return "size out of supported range";
+        default: return "unknown status";
+    }
+}
+
+const char *bloomhip_last_error(void) { return g_last_error.c_str(); }
+
+int bloomhip_device_count(int *count) {
+    g_last_error.clear();
+    if (!count) return BLOOMHIP_EINVAL;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail_hip(e, "hipGetDeviceCount");
+    }
+    *count = n;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_m_bits(int64_t max_size, float bits_per_entry, uint64_t *m_out) {
+    g_last_error.clear();
+    // Run::Run: bloom_filter(max_size * bf_bits_per_entry) — long * float is a
+    // float product, truncated to long by BloomFilter(long).  src/run.cpp:13-15
+    if (!m_out) return BLOOMHIP_EINVAL;
+    const float f = (float)max_size * bits_per_entry;
+    if (std::isnan(f) || f < 1.0f) return BLOOMHIP_EINVAL;  // reference: m==0 -> SIGFPE
+    if (f >= 9.2233720368547758e18f) return BLOOMHIP_ERANGE;
+    *m_out = (uint64_t)(int64_t)f;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_create(int device, uint64_t m_bits, bloomhip_filter **out) {
+    g_last_error.clear();
+    if (!out || m_bits == 0) return BLOOMHIP_EINVAL;
+    *out = nullptr;
+    if (m_bits > (1ull << 46)) return BLOOMHIP_ERANGE;  // 8 TiB of bits: beyond one GPU
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return BLOOMHIP_ENODEV;
+    DeviceGuard g(device);
+    if (!g.ok) return fail_hip(hipErrorInvalidDevice, "hipSetDevice");
+    auto *f = new bloomhip_filter();
+    f->device = device;
+    f->m = m_bits;
+    f->nwords64 = (m_bits + 63) / 64;
+    f->mp = make_mod_params(m_bits);
+    hipError_t e = hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&f->d_words, f->nwords64 * 8);
+    if (e == hipSuccess) e = hipMemsetAsync(f->d_words, 0, f->nwords64 * 8, f->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(f->stream);
+    if (e != hipSuccess) {
+        int rc = fail_hip(e, "bloomhip_create");
+        if (f->d_words) (void)hipFree(f->d_words);
+        if (f->stream) (void)hipStreamDestroy(f->stream);
+        delete f;
+        return rc;
+    }
+    *out = f;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_destroy(bloomhip_filter *f) {
+    g_last_error.clear();
+    if (!f) return BLOOMHIP_EINVAL;
+    DeviceGuard g(f->device);
+    (void)hipStreamSynchronize(f->stream);
+    for (auto &p : f->pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto e : f->spare_events) (void)hipEventDestroy(e);
+    if (f->d_words) (void)hipFree(f->d_words);
+    if (f->d_stage) (void)hipFree(f->d_stage);
+    if (f->d_out_stage) (void)hipFree(f->d_out_stage);
+    if (f->d_bins) (void)hipFree(f->d_bins);
+    if (f->d_counts) (void)hipFree(f->d_counts);
+    (void)hipStreamDestroy(f->stream);
+    delete f;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_size(const bloomhip_filter *f, uint64_t *m_out) {
+    g_last_error.clear();
+    if (!f || !m_out) return BLOOMHIP_EINVAL;
+    *m_out = f->m;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_nwords(const bloomhip_filter *f, uint64_t *nwords_out) {
+    g_last_error.clear();
+    if (!f || !nwords_out) return BLOOMHIP_EINVAL;
+    *nwords_out = f->nwords64;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_device(const bloomhip_filter *f, int *device_out) {
+    g_last_error.clear();
+    if (!f || !device_out) return BLOOMHIP_EINVAL;
+    *device_out = f->device;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_device_words(const bloomhip_filter *f, void **dptr_out) {
+    g_last_error.clear();
+    if (!f || !dptr_out) return BLOOMHIP_EINVAL;
+    *dptr_out = f->d_words;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_stream(const bloomhip_filter *f, void **stream_out) {
+    g_last_error.clear();
+    if (!f || !stream_out) return BLOOMHIP_EINVAL;
+    *stream_out = f->stream;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_clear(bloomhip_filter *f, void *stream) {
+    g_last_error.clear();
+    if (!f) return BLOOMHIP_EINVAL;
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    hipStream_t s = pick_stream(f, stream);
+    hipError_t e = timed(f, SLOT_CLEAR, s,
+                         [&] { return hipMemsetAsync(f->d_words, 0, f->nwords64 * 8, s); });
+    if (e != hipSuccess) return fail_hip(e, "hipMemsetAsync(bitmap)");
+    f->known_zero = true;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_set_batch(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
+                       int keys_on_device, void *stream) {
+    if (!f) return BLOOMHIP_EINVAL;
+    if (n == 0) return BLOOMHIP_OK;
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    hipStream_t s = pick_stream(f, stream);
+    KeySpan ks{};
+    int rc = device_keys(f, keys, n, stride_bytes, keys_on_device, s, &ks);
+    if (rc) return rc;
+    const int strategy = resolve_strategy(f, n);
+    if (!strategy_supported(f, strategy)) return BLOOMHIP_EINVAL;
+    hipError_t e = hipSuccess;
+    switch (strategy) {
+        case BLOOMHIP_BUILD_LDS:
+            e = timed(f, SLOT_LDS, s, [&] { return launch_build_lds(ks, f->mp, f->d_words, s); });
+            break;
+        case BLOOMHIP_BUILD_PARTITION:
+            rc = run_partition(f, ks, s);
+            if (rc) return rc;
+            break;
+        default:
+            e = timed(f, SLOT_ATOMIC, s,
+                      [&] { return launch_build_atomic(ks, f->mp, f->d_words, s); });
+            break;
+    }
+    if (e != hipSuccess) return fail_hip(e, "build kernel launch");
+    f->known_zero = false;
+    if (!keys_on_device) HIP_TRY(hipStreamSynchronize(s));
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const void *keys, size_t n,
+                        size_t stride_bytes, int keys_on_device, uint64_t *out_packed,
+                        int out_on_device, void *stream) {
+    if (!filters || nf <= 0 || !out_packed) return BLOOMHIP_EINVAL;
+    for (int j = 0; j < nf; j++)
+        if (!filters[j] || filters[j]->device != filters[0]->device) return BLOOMHIP_EINVAL;
+    if (n == 0) return BLOOMHIP_OK;
+    // Staging and profiling state live on the first handle.
+    bloomhip_filter *f0 = const_cast<bloomhip_filter *>(filters[0]);
+    DeviceGuard g(f0->device);
+    std::lock_guard<std::mutex> lk(f0->mu);
+    hipStream_t s = pick_stream(f0, stream);
+    KeySpan ks{};
+    int rc = device_keys(f0, keys, n, stride_bytes, keys_on_device, s, &ks);
+    if (rc) return rc;
+    const size_t nw = (n + 63) / 64;
+    const size_t out_bytes = (size_t)nf * nw * 8;
+    uint64_t *dout = out_packed;
+    if (!out_on_device) {
+        HIP_TRY(grow(&f0->d_out_stage, &f0->out_stage_bytes, out_bytes));
+        dout = reinterpret_cast<uint64_t *>(f0->d_out_stage);
+    }
+    for (int j0 = 0; j0 < nf; j0 += kMaxProbeFilters) {
+        ProbeTable t{};
+        t.nf = std::min(nf - j0, kMaxProbeFilters);
+        for (int j = 0; j < t.nf; j++) {
+            t.words[j] = filters[j0 + j]->d_words;
+            t.mp[j] = filters[j0 + j]->mp;
+        }
+        hipError_t e = timed(f0, SLOT_PROBE, s,
+                             [&] { return launch_probe(ks, t, dout + (size_t)j0 * nw, nw, s); });
+        if (e != hipSuccess) return fail_hip(e, "k_probe launch");
+    }
+    if (!out_on_device) {
+        hipError_t e = timed(f0, SLOT_COPY, s, [&] {
+            return hipMemcpyAsync(out_packed, dout, out_bytes, hipMemcpyDeviceToHost, s);
+        });
+        if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(results D2H)");
+    }
+    if (!keys_on_device || !out_on_device) HIP_TRY(hipStreamSynchronize(s));
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_set(bloomhip_filter *f, int32_t key) {
+    g_last_error.clear();
+    return bloomhip_set_batch(f, &key, 1, sizeof key, 0, nullptr);
+}
+
+int bloomhip_is_set(const bloomhip_filter *f, int32_t key, int *hit_out) {
+    g_last_error.clear();
+    if (!f || !hit_out) return BLOOMHIP_EINVAL;
+    uint64_t word = 0;
+    int rc = bloomhip_test_batch(&f, 1, &key, 1, sizeof key, 0, &word, 0, nullptr);
+    if (rc) return rc;
+    *hit_out = (int)(word & 1u);
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_download(const bloomhip_filter *f, uint64_t *words, size_t nwords, void *stream) {
+    g_last_error.clear();
+    if (!f || !words || nwords != f->nwords64) return BLOOMHIP_EINVAL;
+    DeviceGuard g(f->device);
+    hipStream_t s = pick_stream(f, stream);
+    HIP_TRY(hipMemcpyAsync(words, f->d_words, nwords * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_upload(bloomhip_filter *f, const uint64_t *words, size_t nwords, void *stream) {
+    g_last_error.clear();
+    if (!f || !words || nwords != f->nwords64) return BLOOMHIP_EINVAL;
+    const unsigned tail = (unsigned)(f->m % 64);
+    if (tail && (words[nwords - 1] >> tail) != 0) return BLOOMHIP_EINVAL;  // bits >= m
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    hipStream_t s = pick_stream(f, stream);
+    HIP_TRY(hipMemcpyAsync(f->d_words, words, nwords * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    f->known_zero = false;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_sync(const bloomhip_filter *f, void *stream) {
+    g_last_error.clear();
+    if (!f) return BLOOMHIP_EINVAL;
+    DeviceGuard g(f->device);
+    HIP_TRY(hipStreamSynchronize(pick_stream(f, stream)));
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_set_strategy(bloomhip_filter *f, int strategy) {
+    g_last_error.clear();
+    if (!f || strategy < BLOOMHIP_BUILD_AUTO || strategy > BLOOMHIP_BUILD_PARTITION)
+        return BLOOMHIP_EINVAL;
+    if (strategy != BLOOMHIP_BUILD_AUTO && !strategy_supported(f, strategy)) return BLOOMHIP_EINVAL;
+    std::lock_guard<std::mutex> lk(f->mu);
+    f->strategy = strategy;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_resolve_strategy(const bloomhip_filter *f, size_t n, int *strategy_out) {
+    g_last_error.clear();
+    if (!f || !strategy_out) return BLOOMHIP_EINVAL;
+    *strategy_out = resolve_strategy(f, n);
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_profile_enable(bloomhip_filter *f, int enable) {
+    g_last_error.clear();
+    if (!f) return BLOOMHIP_EINVAL;
+    std::lock_guard<std::mutex> lk(f->mu);
+    f->prof = enable != 0;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_profile_read(bloomhip_filter *f, int slot, const char **name_out,
+                          uint64_t *launches_out, double *ms_out) {
+    if (!f || slot < 0 || slot >= BLOOMHIP_PROF_SLOTS) return BLOOMHIP_EINVAL;
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    int rc = harvest_profile(f);
+    if (rc) return rc;
+    if (name_out) *name_out = kSlotNames[slot];
+    if (launches_out) *launches_out = f->prof_launches[slot];
+    if (ms_out) *ms_out = f->prof_ms[slot];
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_profile_reset(bloomhip_filter *f) {
+    g_last_error.clear();
+    if (!f) return BLOOMHIP_EINVAL;
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    int rc = harvest_profile(f);
+    for (int i = 0; i < BLOOMHIP_PROF_SLOTS; i++) {
+        f->prof_ms[i] = 0.0;
+        f->prof_launches[i] = 0;
+    }
+    return rc;
+}
+
+int bloomhip_host_positions(uint64_t m, const int32_t *keys, size_t n, uint64_t *out) {
+    g_last_error.clear();
+    if (m == 0 || (n && (!keys || !out))) return BLOOMHIP_EINVAL;
+    const ModParams mp = make_mod_params(m);
+    for (size_t i = 0; i < n; i++) positions3(keys[i], mp, out + 3 * i);
+    return BLOOMHIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,113 @@
+// bloom_math.h — the position arithmetic of the reference filter, written once
+// for both the gfx950 kernels and the host self-test hook.
+//
+// Reference (jackdent/cs265-lsm-tree):
+//   hash_1  src/bloom_filter.cpp:8-20    hash_2  :22-34    hash_3  :36-47
+//   input  `uint64_t key; key = k;`  — the int32 key SIGN-EXTENDED to 64 bits
+//   output `key % table.size()`      — full 64-bit unsigned remainder by m
+//
+// The remainder is the expensive part on a GPU (no integer divide).  For
+// m < 2^32 (every filter up to 512 MiB) it is computed exactly with two
+// multiplies and no division:
+//   1. fold the high word:   y = xh * (2^32 mod m) + xl        (y ≡ x mod m, y < m * 2^32)
+//   2. one 2-by-1 word division by the normalised divisor d = m << l using the
+//      precomputed reciprocal v = floor((2^64-1)/d) - 2^32 (Möller & Granlund,
+//      "Improved division by invariant integers", IEEE TC 2011, Alg. 4),
+//      keeping only the remainder.
+// Larger m falls back to the compiler's 64-bit remainder (exact, slower).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bloomhip {
+
+#define BH_HD __host__ __device__ __forceinline__
+
+// ---- the three reference hashes, before the modulo --------------------------
+BH_HD uint64_t raw_hash1(int32_t k) {  // src/bloom_filter.cpp:8-20
+    uint64_t x = (uint64_t)(int64_t)k;
+    x = ~x + (x << 15);
+    x = x ^ (x >> 12);
+    x = x + (x << 2);
+    x = x ^ (x >> 4);
+    x = x * 2057u;
+    x = x ^ (x >> 16);
+    return x;
+}
+
+BH_HD uint64_t raw_hash2(int32_t k) {  // src/bloom_filter.cpp:22-34
+    uint64_t x = (uint64_t)(int64_t)k;
+    x = (x + 0x7ed55d16u) + (x << 12);
+    x = (x ^ 0xc761c23cu) ^ (x >> 19);
+    x = (x + 0x165667b1u) + (x << 5);
+    x = (x + 0xd3a2646cu) ^ (x << 9);
+    x = (x + 0xfd7046c5u) + (x << 3);
+    x = (x ^ 0xb55a4f09u) ^ (x >> 16);
+    return x;
+}
+
+BH_HD uint64_t raw_hash3(int32_t k) {  // src/bloom_filter.cpp:36-47
+    uint64_t x = (uint64_t)(int64_t)k;
+    x = (x ^ 61u) ^ (x >> 16);
+    x = x + (x << 3);
+    x = x ^ (x >> 4);
+    x = x * 0x27d4eb2du;
+    x = x ^ (x >> 15);
+    return x;
+}
+
+// ---- exact x % m -------------------------------------------------------------
+struct ModParams {
+    uint64_t m;   // table.size()
+    uint32_t R;   // 2^32 mod m                      (fast path)
+    uint32_t dn;  // m << l, top bit set             (fast path)
+    uint32_t v;   // floor((2^64-1)/dn) - 2^32       (fast path)
+    uint32_t l;   // leading zeros of m as a u32     (fast path)
+    uint32_t fast;  // 1 when m <= 0xFFFFFFFF
+    uint32_t pad;
+};
+
+// Host-side precomputation (m >= 1).
+inline ModParams make_mod_params(uint64_t m) {
+    ModParams p{};
+    p.m = m;
+    if (m >= 1 && m <= 0xFFFFFFFFull) {
+        uint32_t m32 = (uint32_t)m;
+        uint32_t l = (uint32_t)__builtin_clz(m32);
+        uint32_t dn = m32 << l;
+        p.fast = 1;
+        p.l = l;
+        p.dn = dn;
+        p.v = (uint32_t)(~0ull / dn - (1ull << 32));
+        p.R = (uint32_t)((1ull << 32) % m);
+    }
+    return p;
+}
+
+// x % m for m < 2^32 (p.fast).  Returns the remainder as u32.
+BH_HD uint32_t mod_fast(uint64_t x, const ModParams &p) {
+    const uint32_t xh = (uint32_t)(x >> 32), xl = (uint32_t)x;
+    const uint64_t y = (uint64_t)xh * p.R + xl;   // < m * 2^32, so u below < dn * 2^32
+    const uint64_t u = y << p.l;
+    const uint32_t u1 = (uint32_t)(u >> 32), u0 = (uint32_t)u;
+    const uint64_t q = (uint64_t)p.v * u1 + u;    // (q1, q0) = v*u1 + (u1, u0); < 2^64
+    const uint32_t q1 = (uint32_t)(q >> 32) + 1u;
+    const uint32_t q0 = (uint32_t)q;
+    uint32_t r = u0 - q1 * p.dn;
+    if (r > q0) r += p.dn;
+    if (r >= p.dn) r -= p.dn;
+    return r >> p.l;
+}
+
+BH_HD uint64_t mod_any(uint64_t x, const ModParams &p) {
+    return p.fast ? (uint64_t)mod_fast(x, p) : x % p.m;
+}
+
+BH_HD void positions3(int32_t k, const ModParams &p, uint64_t out[3]) {
+    out[0] = mod_any(raw_hash1(k), p);
+    out[1] = mod_any(raw_hash2(k), p);
+    out[2] = mod_any(raw_hash3(k), p);
+}
+
+}  // namespace bloomhip

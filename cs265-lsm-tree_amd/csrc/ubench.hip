@@ -1,0 +1,105 @@
+// ubench.hip — micro-benchmarks that price the primitives the Bloom kernels
+// are built from on gfx950: random 4-B global atomicOr (agent vs workgroup
+// scope), random 4-B gathers, random LDS ds_or, and the exact hash+mod
+// arithmetic alone.  Not part of the product path; used by
+// tools/ubench.py to pick build strategies.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bloom_math.h"
+
+using namespace bloomhip;
+
+namespace {
+
+__device__ __forceinline__ uint32_t xorshift(uint32_t &s) {
+    s ^= s << 13;
+    s ^= s >> 17;
+    s ^= s << 5;
+    return s;
+}
+
+template <int SCOPE>
+__global__ void ub_atomic_or(uint32_t *words, uint32_t nwords, int iters) {
+    uint32_t s = 0x9E3779B9u ^ (blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u;
+    for (int i = 0; i < iters; i++) {
+        const uint32_t r = xorshift(s);
+        const uint32_t w = (uint32_t)(((uint64_t)r * nwords) >> 32);
+        __hip_atomic_fetch_or(words + w, 1u << (r & 31), __ATOMIC_RELAXED, SCOPE);
+    }
+}
+
+__global__ void ub_gather(const uint32_t *words, uint32_t nwords, int iters, uint32_t *sink) {
+    uint32_t s = 0x9E3779B9u ^ (blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u;
+    uint32_t acc = 0;
+    for (int i = 0; i < iters; i++) {
+        const uint32_t r = xorshift(s);
+        const uint32_t w = (uint32_t)(((uint64_t)r * nwords) >> 32);
+        acc += words[w];
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+__global__ void ub_lds_or(int iters, uint32_t *sink) {
+    extern __shared__ uint32_t seg[];
+    for (int i = threadIdx.x; i < 16384; i += blockDim.x) seg[i] = 0;
+    __syncthreads();
+    uint32_t s = 0x9E3779B9u ^ (blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u;
+    for (int i = 0; i < iters; i++) {
+        const uint32_t r = xorshift(s);
+        atomicOr(&seg[r >> 18], 1u << (r & 31));
+    }
+    __syncthreads();
+    if (seg[threadIdx.x] == 0x12345678u) sink[0] = 1;
+}
+
+__global__ void ub_hash(ModParams mp, int iters, uint32_t *sink) {
+    uint32_t acc = 0;
+    int32_t k = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u);
+    for (int i = 0; i < iters; i++) {
+        acc ^= mod_fast(raw_hash1(k), mp) + mod_fast(raw_hash2(k), mp) + mod_fast(raw_hash3(k), mp);
+        k += 0x9E3779B9;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+__global__ void ub_rawhash(int iters, uint32_t *sink) {
+    uint64_t acc = 0;
+    int32_t k = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u);
+    for (int i = 0; i < iters; i++) {
+        acc ^= raw_hash1(k) + raw_hash2(k) + raw_hash3(k);
+        k += 0x9E3779B9;
+    }
+    if (acc == 0x12345678u) sink[0] = (uint32_t)acc;
+}
+
+__global__ void ub_stream(const uint4 *buf, size_t n16, uint32_t *sink) {
+    uint32_t acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 v = buf[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+}  // namespace
+
+extern "C" int ubench_run(int which, void *dbuf, size_t bytes, uint64_t m, int grid, int block,
+                          int iters, void *stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    uint32_t *w = reinterpret_cast<uint32_t *>(dbuf);
+    const uint32_t nwords = (uint32_t)(bytes / 4 - 1);  // last word is the sink
+    uint32_t *sink = w + nwords;
+    switch (which) {
+        case 0: ub_atomic_or<__HIP_MEMORY_SCOPE_AGENT><<<grid, block, 0, s>>>(w, nwords, iters); break;
+        case 1: ub_atomic_or<__HIP_MEMORY_SCOPE_WORKGROUP><<<grid, block, 0, s>>>(w, nwords, iters); break;
+        case 2: ub_gather<<<grid, block, 0, s>>>(w, nwords, iters, sink); break;
+        case 3: ub_lds_or<<<grid, block, 65536, s>>>(iters, sink); break;
+        case 4: ub_hash<<<grid, block, 0, s>>>(make_mod_params(m), iters, sink); break;
+        case 5: ub_rawhash<<<grid, block, 0, s>>>(iters, sink); break;
+        case 6: ub_stream<<<grid, block, 0, s>>>(reinterpret_cast<const uint4 *>(dbuf), bytes / 16 - 1, sink); break;
+        default: return -22;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}

@@ -1,0 +1,145 @@
+/*
+ * bloomhip.h — C ABI of the MI355X (gfx950) Bloom-filter engine.
+ *
+ * Drop-in for the set/test surface of jackdent/cs265-lsm-tree
+ * src/bloom_filter.{h,cpp}:
+ *
+ *   class BloomFilter {                       src/bloom_filter.h:6-15
+ *       boost::dynamic_bitset<> table;        src/bloom_filter.h:7
+ *       uint64_t hash_1/2/3(KEY_t) const;     src/bloom_filter.h:8-10, .cpp:8-47
+ *     public:
+ *       BloomFilter(long length);             src/bloom_filter.h:12
+ *       void set(KEY_t);                      src/bloom_filter.cpp:49-53
+ *       bool is_set(KEY_t) const;             src/bloom_filter.cpp:55-59
+ *   };
+ *
+ * and for its sizing in Run::Run (src/run.cpp:13-15).  Results are bit-exact
+ * with the reference: the same bitmap (dynamic_bitset block layout, bit i in
+ * 64-bit block i/64 at bit i%64) after the same keys are set, and the same
+ * is_set booleans.  k = 3 with the reference's three fixed hashes.
+ *
+ * Conventions
+ *   - Plain C types only; `void *stream` is a hipStream_t (NULL = the filter's
+ *     own stream).  No HIP or torch headers are needed to bind this ABI.
+ *   - Every entry point returns an int status: 0 on success, a negative
+ *     errno-style code on failure; nothing throws across the ABI.  The
+ *     reference has no error path at all (m == 0 is a SIGFPE there,
+ *     src/bloom_filter.cpp:19); here m == 0 is rejected with BLOOMHIP_EINVAL.
+ *   - A handle owns one device bitmap on one device.  Calls on a handle are
+ *     ordered on the stream they are given; different handles may be driven
+ *     from different host threads (one per GPU for per-run sharding).
+ *   - Device-resident calls (keys_on_device = 1, out_on_device = 1) are
+ *     asynchronous.  A call given any HOST buffer synchronises the stream
+ *     before it returns, so host buffers may be reused immediately (the
+ *     reference's calls are synchronous, src/run.cpp:93,162).
+ *   - Keys are KEY_t = int32_t (src/types.h:4) read at `stride_bytes`
+ *     (4 for a packed key vector, 8 for entry_t runs, src/types.h:14-22).
+ */
+#ifndef BLOOMHIP_H
+#define BLOOMHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLOOMHIP_ABI_VERSION 1
+
+#define BLOOMHIP_OK 0
+#define BLOOMHIP_EIO (-5)     /* HIP runtime error; see bloomhip_last_error() */
+#define BLOOMHIP_ENOMEM (-12) /* device allocation failed */
+#define BLOOMHIP_ENODEV (-19) /* no such device / no GPU */
+#define BLOOMHIP_EINVAL (-22) /* bad argument (m == 0, NULL, bad stride...) */
+#define BLOOMHIP_ERANGE (-34) /* size out of supported range */
+
+/* Build strategies for bloomhip_set_batch (bloomhip_set_strategy). */
+#define BLOOMHIP_BUILD_AUTO 0      /* pick by m and n (default) */
+#define BLOOMHIP_BUILD_ATOMIC 1    /* one pass, global atomicOr per bit */
+#define BLOOMHIP_BUILD_LDS 2       /* private LDS bitmap per workgroup (m/8 <= LDS) */
+#define BLOOMHIP_BUILD_PARTITION 3 /* hash+bin pass, then LDS segment pass */
+
+typedef struct bloomhip_filter bloomhip_filter;
+
+int bloomhip_abi_version(void);
+const char *bloomhip_strerror(int status);
+/* Text of the last HIP error seen by this host thread ("" if none). */
+const char *bloomhip_last_error(void);
+int bloomhip_device_count(int *count);
+
+/* m = (long)((float)max_size * bits_per_entry): Run::Run's sizing of its
+ * filter, evaluated in float exactly as src/run.cpp:13-15 does. */
+int bloomhip_m_bits(int64_t max_size, float bits_per_entry, uint64_t *m_out);
+
+/* BloomFilter(long length): an all-zero filter of m_bits bits on `device`.
+ * src/bloom_filter.h:12.  m_bits must be >= 1. */
+int bloomhip_create(int device, uint64_t m_bits, bloomhip_filter **out);
+int bloomhip_destroy(bloomhip_filter *f);
+
+/* table.size() (src/bloom_filter.cpp:19) and the number of 64-bit blocks. */
+int bloomhip_size(const bloomhip_filter *f, uint64_t *m_out);
+int bloomhip_nwords(const bloomhip_filter *f, uint64_t *nwords_out);
+int bloomhip_device(const bloomhip_filter *f, int *device_out);
+/* Device address of the bitmap (ceil(m/64) uint64 blocks), for zero-copy
+ * interop.  Valid until bloomhip_destroy. */
+int bloomhip_device_words(const bloomhip_filter *f, void **dptr_out);
+/* The handle's own stream (used when a call is given stream = NULL). */
+int bloomhip_stream(const bloomhip_filter *f, void **stream_out);
+
+/* Reset every bit to 0. */
+int bloomhip_clear(bloomhip_filter *f, void *stream);
+
+/* BloomFilter::set for keys[0..n): src/bloom_filter.cpp:49-53, as called per
+ * written entry by Run::put (src/run.cpp:162) during a flush
+ * (src/lsm_tree.cpp:127-129) or compaction (src/lsm_tree.cpp:81-88). */
+int bloomhip_set_batch(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
+                       int keys_on_device, void *stream);
+
+/* BloomFilter::is_set of every key against each of nf filters
+ * (src/bloom_filter.cpp:55-59; Run::get's probe, src/run.cpp:93, over the
+ * runs a GET visits, src/lsm_tree.cpp:180-212).  All filters must live on
+ * one device.  Result bit i%64 of out_packed[j*ceil(n/64) + i/64] is
+ * is_set(key i) for filters[j]; bits past n in the last word are 0. */
+int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const void *keys,
+                        size_t n, size_t stride_bytes, int keys_on_device,
+                        uint64_t *out_packed, int out_on_device, void *stream);
+
+/* Scalar compatibility entry points (one key; synchronous). */
+int bloomhip_set(bloomhip_filter *f, int32_t key);
+int bloomhip_is_set(const bloomhip_filter *f, int32_t key, int *hit_out);
+
+/* Persistence: copy the bitmap out/in as ceil(m/64) uint64 blocks in the
+ * reference's dynamic_bitset layout.  Host buffers; synchronous.  Upload
+ * rejects blocks with bits set at positions >= m. */
+int bloomhip_download(const bloomhip_filter *f, uint64_t *words, size_t nwords, void *stream);
+int bloomhip_upload(bloomhip_filter *f, const uint64_t *words, size_t nwords, void *stream);
+
+/* Wait for all work queued on `stream` (NULL: the filter's stream). */
+int bloomhip_sync(const bloomhip_filter *f, void *stream);
+
+/* Build strategy override (BLOOMHIP_BUILD_*); AUTO by default. */
+int bloomhip_set_strategy(bloomhip_filter *f, int strategy);
+/* Strategy AUTO resolved for a batch of n keys on this filter. */
+int bloomhip_resolve_strategy(const bloomhip_filter *f, size_t n, int *strategy_out);
+
+/* Per-kernel device timing.  While enabled, every kernel the handle launches
+ * is bracketed by HIP events on its stream; bloomhip_profile_read returns,
+ * for kernel slot `slot` (0..BLOOMHIP_PROF_SLOTS-1), its name, launch count
+ * and summed device milliseconds (it synchronises the stream). */
+#define BLOOMHIP_PROF_SLOTS 8
+int bloomhip_profile_enable(bloomhip_filter *f, int enable);
+int bloomhip_profile_read(bloomhip_filter *f, int slot, const char **name_out,
+                          uint64_t *launches_out, double *ms_out);
+int bloomhip_profile_reset(bloomhip_filter *f);
+
+/* Self-test hook (no GPU needed): the engine's own position arithmetic —
+ * the same inline functions the kernels run — evaluated on the host.
+ * out[3*i + j] = hash_{j+1}(keys[i]) % m. */
+int bloomhip_host_positions(uint64_t m, const int32_t *keys, size_t n, uint64_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BLOOMHIP_H */

@@ -1,0 +1,198 @@
+"""TEST INFRASTRUCTURE ONLY — parity oracle for the Bloom-filter hot path.
+
+Two independent CPU restatements of the reference filter
+(jackdent/cs265-lsm-tree src/bloom_filter.{h,cpp}):
+
+* ``np_*`` — vectorised numpy uint64 arithmetic (wraps mod 2**64 exactly like
+  the reference's ``uint64_t`` chains, src/bloom_filter.cpp:8-47).
+* ``COracle`` — ctypes binding of ``oracle/bloom_oracle.c`` (scalar C, the CPU
+  baseline timed by bench.py).
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may
+import this module.  The product (``cs265-lsm-tree_amd/``) never does.
+
+Parity is pinned by SURVEY.md §8a/§8c known answers (tests/golden/); the
+reference itself is unbuildable here (needs boost::dynamic_bitset).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+_U64 = np.uint64
+
+
+def _sext(keys) -> np.ndarray:
+    """KEY_t (int32) -> uint64 by sign extension: `uint64_t key; key = k;`
+    src/bloom_filter.cpp:9-11."""
+    k = np.asarray(keys, dtype=np.int32)
+    return k.astype(np.int64).view(np.uint64)
+
+
+def np_raw_hashes(keys) -> np.ndarray:
+    """[n, 3] uint64: hash_1..hash_3 before the modulo (src/bloom_filter.cpp:8-47)."""
+    x0 = _sext(keys)
+    with np.errstate(over="ignore"):
+        # hash_1, src/bloom_filter.cpp:8-20
+        x = ~x0 + (x0 << _U64(15))
+        x = x ^ (x >> _U64(12))
+        x = x + (x << _U64(2))
+        x = x ^ (x >> _U64(4))
+        x = x * _U64(2057)
+        h1 = x ^ (x >> _U64(16))
+        # hash_2, src/bloom_filter.cpp:22-34
+        x = (x0 + _U64(0x7ED55D16)) + (x0 << _U64(12))
+        x = (x ^ _U64(0xC761C23C)) ^ (x >> _U64(19))
+        x = (x + _U64(0x165667B1)) + (x << _U64(5))
+        x = (x + _U64(0xD3A2646C)) ^ (x << _U64(9))
+        x = (x + _U64(0xFD7046C5)) + (x << _U64(3))
+        h2 = (x ^ _U64(0xB55A4F09)) ^ (x >> _U64(16))
+        # hash_3, src/bloom_filter.cpp:36-47
+        x = (x0 ^ _U64(61)) ^ (x0 >> _U64(16))
+        x = x + (x << _U64(3))
+        x = x ^ (x >> _U64(4))
+        x = x * _U64(0x27D4EB2D)
+        h3 = x ^ (x >> _U64(15))
+    return np.stack([h1, h2, h3], axis=1)
+
+
+def np_positions(keys, m: int) -> np.ndarray:
+    """[n, 3] uint64 bit positions: hash_i(k) % table.size() (src/bloom_filter.cpp:19,33,46)."""
+    if m <= 0:
+        raise ValueError("m must be positive (reference divides by table.size())")
+    return np_raw_hashes(keys) % _U64(m)
+
+
+def np_m_bits(max_size: int, bits_per_entry: float) -> int:
+    """Run::Run sizing: `bloom_filter(max_size * bf_bits_per_entry)` with long*float
+    evaluated in float and truncated to long (src/run.cpp:13-15, src/bloom_filter.h:12)."""
+    f = np.float32(np.float32(max_size) * np.float32(bits_per_entry))
+    return int(np.int64(f))
+
+
+def np_words(m: int) -> int:
+    return (m + 63) // 64
+
+
+def np_set_batch(words: np.ndarray, m: int, keys) -> None:
+    """BloomFilter::set over a batch into uint64 blocks (src/bloom_filter.cpp:49-53)."""
+    pos = np_positions(keys, m).reshape(-1)
+    np.bitwise_or.at(words, (pos >> _U64(6)).astype(np.int64),
+                     _U64(1) << (pos & _U64(63)))
+
+
+def np_build(m: int, keys) -> np.ndarray:
+    words = np.zeros(np_words(m), dtype=np.uint64)
+    np_set_batch(words, m, keys)
+    return words
+
+
+def np_test_batch(words: np.ndarray, m: int, keys) -> np.ndarray:
+    """BloomFilter::is_set per key (src/bloom_filter.cpp:55-59) as a bool array."""
+    pos = np_positions(keys, m)
+    bits = (words[(pos >> _U64(6)).astype(np.int64)] >> (pos & _U64(63))) & _U64(1)
+    return bits.all(axis=1)
+
+
+def pack_bools(b: np.ndarray) -> np.ndarray:
+    """bool[n] -> uint64[ceil(n/64)], bit i%64 of word i/64 (little-endian bit order)."""
+    b = np.asarray(b, dtype=bool)
+    n = b.size
+    pad = (-n) % 64
+    bb = np.concatenate([b, np.zeros(pad, dtype=bool)]) if pad else b
+    return np.packbits(bb.reshape(-1, 8), axis=1, bitorder="little").reshape(-1).view(np.uint64).copy()
+
+
+def unpack_bools(packed: np.ndarray, n: int) -> np.ndarray:
+    bits = np.unpackbits(np.asarray(packed, dtype=np.uint64).view(np.uint8), bitorder="little")
+    return bits[:n].astype(bool)
+
+
+# --------------------------------------------------------------------------
+# C restatement (oracle/bloom_oracle.c) via ctypes.
+# --------------------------------------------------------------------------
+def build_c_oracle(force: bool = False) -> str:
+    src = os.path.join(HERE, "bloom_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
+    return LIB_PATH
+
+
+class COracle:
+    """ctypes view of oracle/bloom_oracle.c."""
+
+    def __init__(self):
+        build_c_oracle()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.bo_m_bits.argtypes = [ctypes.c_int64, ctypes.c_float, ctypes.POINTER(ctypes.c_uint64)]
+        L.bo_m_bits.restype = ctypes.c_int
+        L.bo_positions_batch.argtypes = [P, ctypes.c_size_t, ctypes.c_uint64, P]
+        L.bo_raw_batch.argtypes = [P, ctypes.c_size_t, P]
+        L.bo_set_batch.argtypes = [P, ctypes.c_uint64, P, ctypes.c_size_t, ctypes.c_size_t]
+        L.bo_set_batch.restype = ctypes.c_int
+        L.bo_test_batch.argtypes = [P, ctypes.c_uint64, P, ctypes.c_size_t, ctypes.c_size_t, P]
+        L.bo_test_batch.restype = ctypes.c_int
+        L.bo_is_set.argtypes = [P, ctypes.c_uint64, ctypes.c_int32]
+        L.bo_is_set.restype = ctypes.c_int
+        L.bo_popcount.argtypes = [P, ctypes.c_size_t]
+        L.bo_popcount.restype = ctypes.c_uint64
+        self.L = L
+
+    def m_bits(self, max_size: int, bpe: float) -> int:
+        out = ctypes.c_uint64()
+        rc = self.L.bo_m_bits(max_size, bpe, ctypes.byref(out))
+        if rc != 0:
+            raise ValueError(f"bo_m_bits({max_size}, {bpe}) -> {rc}")
+        return out.value
+
+    def positions(self, keys, m: int) -> np.ndarray:
+        k = np.ascontiguousarray(keys, dtype=np.int32)
+        out = np.empty((k.size, 3), dtype=np.uint64)
+        self.L.bo_positions_batch(k.ctypes.data, k.size, m, out.ctypes.data)
+        return out
+
+    def raw(self, keys) -> np.ndarray:
+        k = np.ascontiguousarray(keys, dtype=np.int32)
+        out = np.empty((k.size, 3), dtype=np.uint64)
+        self.L.bo_raw_batch(k.ctypes.data, k.size, out.ctypes.data)
+        return out
+
+    def build(self, m: int, keys, stride: int = 4, n: int | None = None) -> np.ndarray:
+        """Bitmap (uint64 blocks) after set() of every key.  `keys` may be an
+        AoS buffer read at `stride` bytes (entry_t runs: stride 8)."""
+        buf = np.ascontiguousarray(keys)
+        if n is None:
+            n = buf.nbytes // stride
+        words = np.zeros(np_words(m), dtype=np.uint64)
+        rc = self.L.bo_set_batch(words.ctypes.data, m, buf.ctypes.data, n, stride)
+        if rc != 0:
+            raise ValueError(f"bo_set_batch rc={rc}")
+        return words
+
+    def set_into(self, words: np.ndarray, m: int, keys, stride: int = 4) -> None:
+        buf = np.ascontiguousarray(keys)
+        rc = self.L.bo_set_batch(words.ctypes.data, m, buf.ctypes.data, buf.nbytes // stride, stride)
+        if rc != 0:
+            raise ValueError(f"bo_set_batch rc={rc}")
+
+    def test(self, words: np.ndarray, m: int, keys, stride: int = 4) -> np.ndarray:
+        """Packed uint64 results, bit i%64 of word i/64 = is_set(key i)."""
+        buf = np.ascontiguousarray(keys)
+        n = buf.nbytes // stride
+        out = np.zeros((n + 63) // 64, dtype=np.uint64)
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        rc = self.L.bo_test_batch(w.ctypes.data, m, buf.ctypes.data, n, stride, out.ctypes.data)
+        if rc != 0:
+            raise ValueError(f"bo_test_batch rc={rc}")
+        return out
+
+    def popcount(self, words: np.ndarray) -> int:
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        return int(self.L.bo_popcount(w.ctypes.data, w.size))

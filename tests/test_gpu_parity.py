@@ -1,0 +1,276 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the oracle.
+
+Bit-exact: the same bitmap blocks after set_batch, the same packed is_set
+booleans after test_batch.  Small cases compare with the C oracle directly;
+full-size configs compare with the SHA-256 fixtures the pinned oracle wrote
+(tests/golden/pins.json) plus size-independent properties (no false
+negatives, idempotence, order independence, merge = union).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import bloomhip as bh
+from bloom_oracle import unpack_bools
+
+pytestmark = pytest.mark.gpu
+
+STRATEGIES = [bh.BUILD_ATOMIC, bh.BUILD_LDS, bh.BUILD_PARTITION]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def rand_keys(n, seed=0):
+    rng = np.random.default_rng(seed)
+    k = rng.integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32)
+    if n >= 6:
+        k[:6] = [0, -1, 1, 2**31 - 1, -2**31, 13141]
+    return k
+
+
+def supported(f, strategy):
+    try:
+        f.set_strategy(strategy)
+        return True
+    except bh.BloomHipError:
+        return False
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch
+
+
+# ---------------------------------------------------------------- build ----
+@pytest.mark.parametrize("m", [1, 2, 31, 32, 33, 64, 65, 256, 1000, 65_537, 512_000, 524_288,
+                               1_000_003, 4_194_304, 10_485_761, 167_772_160])
+@pytest.mark.parametrize("strategy", STRATEGIES, ids=["atomic", "lds", "partition"])
+def test_build_matches_oracle(coracle, m, strategy):
+    n = 200_000 if m > 100_000 else 5_000
+    keys = rand_keys(n, seed=m % 1000)
+    f = bh.BloomFilter(m)
+    if not supported(f, strategy):
+        pytest.skip("strategy not applicable to this m")
+    f.set_batch(keys)
+    assert (f.words() == coracle.build(m, keys)).all()
+
+
+@pytest.mark.parametrize("strategy", STRATEGIES, ids=["atomic", "lds", "partition"])
+def test_build_device_keys_and_accumulation(coracle, torch_cuda, strategy):
+    torch = torch_cuda
+    m = 4_000_037 if strategy != bh.BUILD_LDS else 400_009
+    a, b = rand_keys(300_000, 1), rand_keys(300_000, 2)
+    f = bh.BloomFilter(m)
+    if not supported(f, strategy):
+        pytest.skip("n/a")
+    f.set_batch(torch.from_numpy(a).cuda())
+    f.sync()
+    f.set_batch(torch.from_numpy(b).cuda())   # second batch ORs into the first
+    f.sync()
+    assert (f.words() == coracle.build(m, np.concatenate([a, b]))).all()
+
+
+def test_build_generic_mod_path_m_above_2_32(coracle):
+    m = 2**32 + 1_000_003    # 512 MiB bitmap; 64-bit remainder path
+    keys = rand_keys(100_000, 9)
+    f = bh.BloomFilter(m)
+    f.set_batch(keys)
+    ref = coracle.build(m, keys)
+    w = f.words()
+    assert (w == ref).all()
+
+
+def test_entry_t_run_stride8_c1(coracle, golden):
+    """C1: the first flushed run as AoS entry_t (src/types.h:14-22) at stride 8."""
+    from bloomhip import workloads as W
+    run, m = W.c1_run()
+    ref = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__),
+                                             "golden", "c1_bitmap.npy"))
+    for strategy in STRATEGIES:
+        f = bh.BloomFilter(m)
+        if not supported(f, strategy):
+            continue
+        f.set_batch(run.reshape(-1), n=run.shape[0], stride=8)
+        w = f.words()
+        assert (w == ref).all(), strategy
+        assert sha(w) == golden["oracle"]["c1"]["sha256"]
+
+
+def test_unaligned_and_strided_keys(coracle):
+    keys = rand_keys(100_003, 4)
+    m = 1_048_583
+    buf = np.zeros(keys.size + 1, dtype=np.int32)
+    buf[1:] = keys                            # 4-byte offset: not 16-byte aligned
+    f = bh.BloomFilter(m)
+    f.set_batch(buf[1:])
+    assert (f.words() == coracle.build(m, keys)).all()
+    wide = np.zeros((keys.size, 3), dtype=np.int32)  # stride 12
+    wide[:, 0] = keys
+    g = bh.BloomFilter(m)
+    g.set_batch(wide.reshape(-1), n=keys.size, stride=12)
+    assert (g.words() == f.words()).all()
+
+
+def test_empty_and_single_key(coracle):
+    f = bh.BloomFilter(1000)
+    f.set_batch(np.zeros(0, dtype=np.int32))
+    assert not f.words().any()
+    f.set(-2**31)
+    assert (f.words() == coracle.build(1000, np.array([-2**31], np.int32))).all()
+    assert f.is_set(-2**31)
+
+
+def test_adversarial_single_key_overflows_bins(coracle):
+    """All positions in three segments: bins overflow and spill to atomics."""
+    keys = np.full(3_000_000, 777, dtype=np.int32)
+    keys[::1000] = np.arange(3000, dtype=np.int32)
+    m = 167_772_160
+    f = bh.BloomFilter(m)
+    f.set_strategy(bh.BUILD_PARTITION)
+    f.set_batch(keys)
+    assert (f.words() == coracle.build(m, keys)).all()
+
+
+def test_order_independence_and_idempotence():
+    keys = rand_keys(500_000, 12)
+    m = 5_000_011
+    f = bh.BloomFilter(m)
+    f.set_batch(keys)
+    w1 = f.words()
+    g = bh.BloomFilter(m)
+    g.set_batch(keys[::-1].copy())
+    g.set_batch(keys)                         # idempotent
+    assert (g.words() == w1).all()
+
+
+def test_upload_download_roundtrip_and_validation():
+    m = 100_003
+    keys = rand_keys(10_000, 13)
+    f = bh.BloomFilter(m)
+    f.set_batch(keys)
+    w = f.words()
+    g = bh.BloomFilter(m)
+    g.load_words(w)
+    assert (g.words() == w).all()
+    assert unpack_bools(bh.test_batch([g], keys)[0], keys.size).all()
+    bad = w.copy()
+    bad[-1] |= np.uint64(1) << np.uint64(63)   # bit >= m
+    with pytest.raises(bh.BloomHipError):
+        g.load_words(bad)
+
+
+def test_clear_resets():
+    f = bh.BloomFilter(1_000_000)
+    f.set_batch(rand_keys(1000, 1))
+    f.clear()
+    assert not f.words().any()
+
+
+# ---------------------------------------------------------------- probe ----
+@pytest.mark.parametrize("m", [1, 64, 65, 1000, 655_360, 1_000_003, 167_772_160, 2**32 + 15])
+def test_probe_matches_oracle(coracle, m):
+    keys = rand_keys(100_000 if m < 2**32 else 20_000, 21)
+    f = bh.BloomFilter(m)
+    f.set_batch(keys)
+    probe = np.concatenate([keys[:30_000], rand_keys(70_001, 22)])
+    got = bh.test_batch([f], probe)[0]
+    assert (got == coracle.test(coracle.build(m, keys), m, probe)).all()
+    assert unpack_bools(got, probe.size)[:min(30_000, keys.size)].all()   # no false negatives
+
+
+def test_probe_many_filters_chunks_past_16(coracle):
+    rng = np.random.default_rng(3)
+    filters, refs = [], []
+    for j in range(20):
+        m = int(rng.integers(1000, 3_000_000))
+        keys = rand_keys(20_000, 100 + j)
+        f = bh.BloomFilter(m)
+        f.set_batch(keys)
+        filters.append(f)
+        refs.append((m, coracle.build(m, keys)))
+    probe = rand_keys(50_017, 99)
+    probe[:20_000] = rand_keys(20_000, 105)
+    got = bh.test_batch(filters, probe)
+    for j, (m, w) in enumerate(refs):
+        assert (got[j] == coracle.test(w, m, probe)).all(), j
+
+
+def test_probe_device_buffers_and_strides(coracle, torch_cuda):
+    torch = torch_cuda
+    m = 2_000_003
+    keys = rand_keys(64 * 1000 + 37, 31)
+    f = bh.BloomFilter(m)
+    f.set_batch(keys)
+    ref = coracle.test(coracle.build(m, keys), m, keys)
+    dk = torch.from_numpy(keys).cuda()
+    dout = torch.zeros((1, (keys.size + 63) // 64), dtype=torch.int64, device="cuda")
+    bh.test_batch([f], dk, out=dout)
+    torch.cuda.synchronize()
+    f.sync()
+    assert (dout.cpu().numpy().view(np.uint64)[0] == ref).all()
+    aos = np.zeros((keys.size, 2), dtype=np.int32)
+    aos[:, 0] = keys
+    got = bh.test_batch([f], aos.reshape(-1), n=keys.size, stride=8)[0]
+    assert (got == ref).all()
+
+
+def test_probe_empty():
+    f = bh.BloomFilter(100)
+    out = bh.test_batch([f], np.zeros(0, dtype=np.int32))
+    assert out.shape == (1, 0)
+
+
+# -------------------------------------------------------- full configs ----
+def test_c2_full_bitmap(golden):
+    from bloomhip import workloads as W
+    keys, m = W.c2()
+    for strategy in STRATEGIES:
+        f = bh.BloomFilter(m)
+        if not supported(f, strategy):
+            continue
+        f.set_batch(keys)
+        w = f.words()
+        assert sha(w) == golden["oracle"]["c2"]["sha256"], strategy
+        assert int(np.unpackbits(w.view(np.uint8)).sum()) == golden["reference"]["c2_popcount"]
+
+
+def test_c3_probe_five_levels(golden):
+    from bloomhip import workloads as W
+    gets, levels = W.c3()
+    filters = []
+    for lvl, keys, m in levels:
+        f = bh.BloomFilter(m)
+        f.set_batch(keys)
+        lv = golden["oracle"]["c3"]["levels"][lvl]
+        assert sha(f.words()) == lv["sha256"], lvl
+        filters.append(f)
+    got = bh.test_batch(filters, gets)
+    for lvl in range(5):
+        lv = golden["oracle"]["c3"]["levels"][lvl]
+        assert sha(got[lvl]) == lv["hits_sha256"], lvl
+        assert int(np.unpackbits(got[lvl].view(np.uint8)).sum()) == golden["reference"]["c3_hits"][lvl]
+
+
+def test_c4_full_bitmap(golden):
+    from bloomhip import workloads as W
+    keys, m = W.c4()
+    f = bh.BloomFilter(m)
+    f.set_batch(keys)
+    w = f.words()
+    assert sha(w) == golden["oracle"]["c4"]["sha256"]
+    # probe property at full size: every inserted key tests positive
+    got = bh.test_batch([f], keys[::97].copy())[0]
+    assert unpack_bools(got, keys[::97].size).all()
+
+
+def test_c5_run0_full_bitmap(golden):
+    from bloomhip import workloads as W
+    keys, m = W.c5_run(0)
+    f = bh.BloomFilter(m)
+    f.set_batch(keys)
+    assert sha(f.words()) == golden["oracle"]["c5"][0]["sha256"]

@@ -1,0 +1,147 @@
+"""Host-side checks of the engine library (CPU only, no kernel launches).
+
+* libbloomhip.so loads and exports every symbol include/*.h declares;
+* the kernels' position arithmetic (bloom_math.h, evaluated on the host via
+  bloomhip_host_positions) equals the oracle for edge and random m;
+* Run::Run sizing (bloomhip_m_bits) and argument validation;
+* the workload generator restatement against independent RNGs.
+"""
+import ctypes
+import glob
+import os
+import re
+
+import numpy as np
+import pytest
+
+import bloomhip as bh
+from bloom_oracle import np_m_bits, np_positions
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(h).read()
+        syms.update(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(bloomhip_\w+)\s*\(", text, re.M))
+    return sorted(syms)
+
+
+def test_library_exports_every_declared_symbol():
+    syms = _declared_symbols()
+    assert len(syms) >= 25
+    L = ctypes.CDLL(bh.LIB_PATH)
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert set(syms) == set(bh.EXPORTED_SYMBOLS)
+
+
+def test_abi_version():
+    assert bh.lib().bloomhip_abi_version() == 1
+
+
+EDGE_M = [1, 2, 3, 31, 32, 33, 63, 64, 65, 255, 256, 257, 1000, 65_536, 524_288, 1_000_003,
+          655_360, 167_772_160, 671_088_640, 2**31 - 1, 2**31, 2**31 + 1, 3_221_225_472,
+          2**32 - 2, 2**32 - 1, 2**32, 2**32 + 1, 2**33 + 5, 2**46]
+
+
+@pytest.fixture(scope="module")
+def fuzz_keys():
+    rng = np.random.default_rng(11)
+    k = rng.integers(-2**31, 2**31, size=40_000, dtype=np.int64).astype(np.int32)
+    k[:8] = [0, -1, 1, 2**31 - 1, -2**31, -2**31 + 1, 13141, -2_652_462]
+    return k
+
+
+@pytest.mark.parametrize("m", EDGE_M)
+def test_engine_mod_arithmetic_edge_m(m, fuzz_keys):
+    assert (bh.host_positions(m, fuzz_keys) == np_positions(fuzz_keys, m)).all()
+
+
+def test_engine_mod_arithmetic_random_m(fuzz_keys):
+    rng = np.random.default_rng(5)
+    ms = np.concatenate([rng.integers(1, 2**32, size=300), rng.integers(1, 2**20, size=100),
+                         (rng.integers(1, 64, size=50) << rng.integers(0, 26, size=50))])
+    for m in ms.tolist():
+        assert (bh.host_positions(int(m), fuzz_keys[:2000]) ==
+                np_positions(fuzz_keys[:2000], int(m))).all(), m
+
+
+def test_m_bits_matches_reference_sizing():
+    rng = np.random.default_rng(2)
+    for size, bpe in [(16_777_217, 10.0), (33_554_431, 0.5), (51_200, 7.7), (512, 0.5)] + [
+            (int(s), float(np.float32(b))) for s, b in zip(rng.integers(1, 2**31, 200),
+                                                          rng.uniform(0.1, 20, 200))]:
+        assert bh.m_bits(size, bpe) == np_m_bits(size, bpe)
+
+
+@pytest.mark.parametrize("size,bpe", [(512, 0.001), (0, 10.0), (100, -1.0), (100, float("nan"))])
+def test_m_bits_rejects_empty_filter(size, bpe):
+    with pytest.raises(bh.BloomHipError) as e:
+        bh.m_bits(size, bpe)
+    assert e.value.status == bh.EINVAL
+
+
+def test_create_rejects_zero_bits():
+    h = ctypes.c_void_p()
+    assert bh.lib().bloomhip_create(0, 0, ctypes.byref(h)) == bh.EINVAL
+
+
+def test_null_arguments_rejected():
+    L = bh.lib()
+    assert L.bloomhip_size(None, None) == bh.EINVAL
+    assert L.bloomhip_set_batch(None, None, 0, 4, 0, None) == bh.EINVAL
+    assert L.bloomhip_test_batch(None, 1, None, 0, 4, 0, None, 0, None) == bh.EINVAL
+    assert L.bloomhip_destroy(None) == bh.EINVAL
+    assert L.bloomhip_host_positions(0, None, 0, None) == bh.EINVAL
+
+
+def test_no_gpu_fails_loudly_not_silently():
+    """Without a device the engine must refuse, never fall back to the CPU."""
+    if bh.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(bh.BloomHipError) as e:
+        bh.BloomFilter(1024)
+    assert e.value.status in (bh.ENODEV, bh.EIO)
+
+
+def test_mt19937_matches_numpy():
+    for seed in (13141, 13142, 0, 5489):
+        ref = np.random.RandomState(seed if seed else 4357).randint(
+            0, 2**32, size=3000, dtype=np.uint64).astype(np.uint32)
+        assert (bh.gen_mt19937(seed, 3000) == ref).all()
+
+
+def test_glibc_rand_matches_libc():
+    libc = ctypes.CDLL("libc.so.6")
+    for seed in (1, 2, 13141):
+        libc.srand(seed)
+        ref = np.array([libc.rand() for _ in range(4000)], dtype=np.int32)
+        assert (bh.gen_glibc_rand(seed, 4000) == ref).all()
+    libc.srand(1)
+
+
+def test_puts_stream_is_even_mt_outputs():
+    keys, vals = bh.gen_puts(13141, 1000, with_vals=True)
+    mt = bh.gen_mt19937(13141, 2000).view(np.int32)
+    assert (keys == mt[0::2]).all() and (vals == mt[1::2]).all()
+
+
+def test_workload_small_stream_shape():
+    puts, gets = bh.gen_workload(13141, 5000, 3000, 0.2, 0.3)
+    assert puts.size == 5000 and gets.size == 3000
+    # A puts-only prefix of the MT stream: puts draw key,value; miss-GETs draw
+    # one value, so every put key is an MT output.
+    mt = set(bh.gen_mt19937(13141, 20000).view(np.int32).tolist())
+    assert set(puts.tolist()) <= mt
+    # ~70% of non-repeated GETs come from earlier puts (miss ratio 0.3).
+    frac = np.isin(gets, puts).mean()
+    assert 0.55 < frac < 0.85
+
+
+def test_c1_run_is_sorted_distinct_prefix():
+    from bloomhip import workloads as W
+    run, m = W.c1_run()
+    assert m == 512_000 and run.shape == (51_200, 2)
+    assert (np.diff(run[:, 0].astype(np.int64)) > 0).all()

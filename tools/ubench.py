@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Prices the gfx950 primitives the Bloom kernels are made of:
+random 4-B global atomicOr (agent / workgroup scope), random 4-B gathers,
+random LDS ds_or, the exact hash+mod arithmetic, and a streaming read.
+Prints one JSON object per measurement."""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = ctypes.CDLL(os.path.join(ROOT, "cs265-lsm-tree_amd", "lib", "libbloomhip_ubench.so"))
+LIB.ubench_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
+                           ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+LIB.ubench_run.restype = ctypes.c_int
+
+
+def timeit(which, buf, nbytes, m, grid, block, iters, reps=5):
+    s = torch.cuda.current_stream()
+    rc = LIB.ubench_run(which, buf.data_ptr(), nbytes, m, grid, block, iters, s.cuda_stream)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        LIB.ubench_run(which, buf.data_ptr(), nbytes, m, grid, block, iters, s.cuda_stream)
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    torch.cuda.set_device(0)
+    grid, block = 2048, 256
+    threads = grid * block
+    out = []
+    for size in [80 << 10, 2 << 20, 20 << 20, 80 << 20, 384 << 20]:
+        buf = torch.zeros(size // 4 + 4, dtype=torch.int32, device="cuda")
+        nb = buf.numel() * 4
+        for which, name, iters in [(0, "atomic_or_agent", 64), (1, "atomic_or_workgroup", 64),
+                                   (2, "gather", 256)]:
+            ms = timeit(which, buf, nb, 0, grid, block, iters)
+            ops = threads * iters
+            out.append({"op": name, "table_bytes": size, "Gops_s": round(ops / ms / 1e6, 2),
+                        "ms": round(ms, 4)})
+            print(json.dumps(out[-1]), flush=True)
+    buf = torch.zeros(1 << 20, dtype=torch.int32, device="cuda")
+    ms = timeit(3, buf, buf.numel() * 4, 0, grid, 1024, 256)
+    print(json.dumps({"op": "lds_or", "Gops_s": round(grid * 1024 * 256 / ms / 1e6, 1),
+                      "ms": round(ms, 4)}), flush=True)
+    for m in [167_772_160, 655_360, 3_221_225_472]:
+        ms = timeit(4, buf, buf.numel() * 4, m, grid, block, 256)
+        print(json.dumps({"op": "hash3+mod_fast", "m": m,
+                          "Gkeys_s": round(threads * 256 / ms / 1e6, 1), "ms": round(ms, 4)}),
+              flush=True)
+    ms = timeit(5, buf, buf.numel() * 4, 0, grid, block, 256)
+    print(json.dumps({"op": "hash3_raw", "Gkeys_s": round(threads * 256 / ms / 1e6, 1),
+                      "ms": round(ms, 4)}), flush=True)
+    big = torch.zeros(1 << 28, dtype=torch.int32, device="cuda")  # 1 GiB
+    ms = timeit(6, big, big.numel() * 4, 0, 4096, 256, 1)
+    print(json.dumps({"op": "stream_read", "GB_s": round(big.numel() * 4 / ms / 1e6, 1),
+                      "ms": round(ms, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
