@@ -84,23 +84,27 @@ def probe_c3(torch, bh, steps, warmup):
     for _ in range(warmup):
         bh.test_batch(filters, dgets, out=dout, stream=s)
     torch.cuda.synchronize()
-    f0 = filters[0]
-    f0.profile(True)
-    f0.profile_reset()
     t0 = time.perf_counter()
     for _ in range(steps):
         bh.test_batch(filters, dgets, out=dout, stream=s)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
-    prof = f0.profile_read()["k_probe"]
+    f0 = filters[0]
+    f0.profile(True)
+    f0.profile_reset()
+    for _ in range(steps):
+        bh.test_batch(filters, dgets, out=dout, stream=s)
+    torch.cuda.synchronize()
+    prof = f0.profile_read()
     f0.profile(False)
-    kms = prof["ms"] / prof["launches"]
+    kms = sum(v["ms"] for k, v in prof.items() if k in ("k_probe", "probe_partitioned")) / steps
     hits = dout.cpu().numpy().view("uint64")
     import numpy as np
     hit_counts = [int(np.unpackbits(hits[j].view(np.uint8)).sum()) for j in range(len(filters))]
     algo = 4 * gets.size + sum((m + 63) // 64 * 8 for _, _, m in levels) + len(levels) * nw * 8
     return {"gkeys_s": round(gets.size / (wall * 1e9), 3),
             "kernel_ms": round(kms, 4), "wall_ms": round(wall * 1e3, 4),
+            "kernels": {k: round(v["ms"] / steps, 4) for k, v in prof.items()},
             "algorithmic_bytes": algo,
             "achieved_GBps": round(algo / (kms * 1e-3) / 1e9, 1),
             "frac": round(algo / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
@@ -134,8 +138,8 @@ def e2e_build(torch, bh, keys_np, m, reps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--strategy", default="auto", choices=["auto", "atomic", "lds", "partition"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -170,12 +174,10 @@ def main():
     resolved = bh.STRATEGY_NAMES[f.resolve_strategy(n)]
     s = torch.cuda.current_stream()
 
-    for _ in range(args.warmup):
-        f.clear(stream=s)
-        f.set_batch(dkeys, stream=s)
+    # Validity: the bitmap a step produces is the oracle-pinned one.
+    f.clear(stream=s)
+    f.set_batch(dkeys, stream=s)
     torch.cuda.synchronize()
-
-    # Validity: the bitmap the timed steps produce is the oracle-pinned one.
     verified = None
     pins_path = os.path.join(ROOT, "tests", "golden", "pins.json")
     if os.path.exists(pins_path):
@@ -193,8 +195,10 @@ def main():
             if not verified:
                 log(f"rank {rank}: BITMAP MISMATCH vs oracle fixture")
 
-    f.profile(True)
-    f.profile_reset()
+    # Warm-up directly before the timed loop (clocks ramp down while idle).
+    for _ in range(args.warmup):
+        f.clear(stream=s)
+        f.set_batch(dkeys, stream=s)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -210,6 +214,16 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # Per-kernel device time: the same K steps again with every launch
+    # bracketed by HIP events on the launch stream (kept out of the timed
+    # loop above so event records do not perturb it).
+    f.profile(True)
+    f.profile_reset()
+    for _ in range(args.steps):
+        f.clear(stream=s)
+        f.set_batch(dkeys, stream=s)
+    torch.cuda.synchronize()
     prof = f.profile_read()
     f.profile(False)
 

@@ -37,6 +37,9 @@ BUILD_AUTO = 0
 BUILD_ATOMIC = 1
 BUILD_LDS = 2
 BUILD_PARTITION = 3
+PROBE_AUTO = 0
+PROBE_GATHER = 1
+PROBE_PARTITION = 2
 STRATEGY_NAMES = {BUILD_AUTO: "auto", BUILD_ATOMIC: "atomic", BUILD_LDS: "lds",
                   BUILD_PARTITION: "partition"}
 PROF_SLOTS = 8
@@ -48,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "bloomhip_nwords", "bloomhip_device", "bloomhip_device_words", "bloomhip_stream",
     "bloomhip_clear", "bloomhip_set_batch", "bloomhip_test_batch", "bloomhip_set",
     "bloomhip_is_set", "bloomhip_download", "bloomhip_upload", "bloomhip_sync",
-    "bloomhip_set_strategy", "bloomhip_resolve_strategy", "bloomhip_profile_enable",
+    "bloomhip_set_strategy", "bloomhip_set_probe_strategy", "bloomhip_resolve_strategy", "bloomhip_profile_enable",
     "bloomhip_profile_read", "bloomhip_profile_reset", "bloomhip_host_positions",
     "bloomhip_gen_mt19937", "bloomhip_gen_glibc_rand", "bloomhip_gen_puts",
     "bloomhip_gen_workload",
@@ -70,6 +73,15 @@ _LIB = None
 def _lib():
     global _LIB
     if _LIB is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64 with the
+        # same SONAME as /opt/rocm's.  Loading torch first makes the loader bind
+        # this library to torch's copy, so device pointers and streams from
+        # torch are valid here; loading ours first would leave torch with a
+        # second runtime that cannot see the GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"bloomhip: {LIB_PATH} is missing — build it with "
@@ -99,6 +111,7 @@ def _lib():
             "bloomhip_upload": (I, [P, P, SZ, P]),
             "bloomhip_sync": (I, [P, P]),
             "bloomhip_set_strategy": (I, [P, I]),
+            "bloomhip_set_probe_strategy": (I, [P, I]),
             "bloomhip_resolve_strategy": (I, [P, SZ, ctypes.POINTER(I)]),
             "bloomhip_profile_enable": (I, [P, I]),
             "bloomhip_profile_read": (I, [P, I, ctypes.POINTER(ctypes.c_char_p), PU64,
@@ -251,6 +264,9 @@ class BloomFilter:
 
     def set_strategy(self, strategy: int) -> None:
         _check(_lib().bloomhip_set_strategy(self._h, strategy), "bloomhip_set_strategy")
+
+    def set_probe_strategy(self, strategy: int) -> None:
+        _check(_lib().bloomhip_set_probe_strategy(self._h, strategy), "bloomhip_set_probe_strategy")
 
     def resolve_strategy(self, n: int) -> int:
         s = ctypes.c_int()

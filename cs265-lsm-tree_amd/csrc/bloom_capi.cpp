@@ -44,6 +44,11 @@ struct DeviceGuard {
     bool ok = false;
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev == dev) {  // common case: nothing to switch or restore
+            prev = -1;
+            ok = true;
+            return;
+        }
         ok = hipSetDevice(dev) == hipSuccess;
     }
     ~DeviceGuard() {
@@ -58,12 +63,12 @@ enum ProfSlot {
     SLOT_PART_BIN = 3,
     SLOT_PART_APPLY = 4,
     SLOT_PROBE = 5,
-    SLOT_COUNTS = 6,
+    SLOT_PROBE_PART = 6,
     SLOT_COPY = 7,
 };
 const char *kSlotNames[BLOOMHIP_PROF_SLOTS] = {
     "clear(memset)",          "k_build_atomic", "k_build_lds",      "k_part_bin",
-    "k_part_apply",           "k_probe",        "part_counts(memset)", "copy",
+    "k_part_apply",           "k_probe",        "probe_partitioned", "copy",
 };
 
 struct PendingTiming {
@@ -81,6 +86,7 @@ struct bloomhip_filter {
     hipStream_t stream = nullptr;
     ModParams mp{};
     int strategy = BLOOMHIP_BUILD_AUTO;
+    int probe_strategy = BLOOMHIP_PROBE_AUTO;
     bool known_zero = true;  // host-side knowledge that every bit is 0
 
     std::mutex mu;  // guards staging, workspace and profiling state
@@ -88,9 +94,12 @@ struct bloomhip_filter {
     size_t stage_bytes = 0;
     void *d_out_stage = nullptr;
     size_t out_stage_bytes = 0;
-    uint32_t *d_bins = nullptr;
+    uint32_t *d_bins = nullptr;    // partition: tile-sorted positions
     size_t bins_bytes = 0;
-    uint32_t *d_counts = nullptr;
+    uint32_t *d_counts = nullptr;  // partition: per-tile run starts
+    size_t counts_bytes = 0;
+    uint8_t *d_res = nullptr;      // partitioned probe: per-key result bytes
+    size_t res_bytes = 0;
 
     bool prof = false;
     uint64_t prof_launches[BLOOMHIP_PROF_SLOTS] = {};
@@ -197,7 +206,7 @@ int resolve_strategy(const bloomhip_filter *f, size_t n) {
     const uint64_t bytes = (f->m + 7) / 8;
     if (bytes <= kLdsBitmapBytes) {
         // Worth a private LDS copy once the batch outweighs the merge.
-        return n >= (size_t)(f->m / 32) ? BLOOMHIP_BUILD_LDS : BLOOMHIP_BUILD_ATOMIC;
+        return n >= (size_t)(f->m / 64) ? BLOOMHIP_BUILD_LDS : BLOOMHIP_BUILD_ATOMIC;
     }
     const uint64_t nbins = (f->m + (1ull << kSegBits) - 1) >> kSegBits;
     if (nbins <= kPartMaxBins && n >= (size_t)nbins * 256) return BLOOMHIP_BUILD_PARTITION;
@@ -214,23 +223,43 @@ int strategy_supported(const bloomhip_filter *f, int strategy) {
     }
 }
 
+// Sizes the partition workspace of `owner` for n keys against filter size m.
+int partition_workspace(bloomhip_filter *owner, uint64_t m, size_t n, PartitionWorkspace *out) {
+    PartitionWorkspace ws{};
+    ws.nbins = (size_t)((m + (1ull << kSegBits) - 1) >> kSegBits);
+    ws.ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
+    size_t nsplit = ws.nbins >= 128 ? 1 : (256 + ws.nbins - 1) / ws.nbins;
+    nsplit = std::min(nsplit, std::max<size_t>(1, ws.ntiles / 8));
+    ws.nsplit = std::max<size_t>(1, nsplit);
+    HIP_TRY(grow(reinterpret_cast<void **>(&owner->d_bins), &owner->bins_bytes,
+                 ws.ntiles * (size_t)kPartTilePos * 4));
+    HIP_TRY(grow(reinterpret_cast<void **>(&owner->d_counts), &owner->counts_bytes,
+                 ws.ntiles * (ws.nbins + 1) * 4));
+    ws.pos = owner->d_bins;
+    ws.run_starts = owner->d_counts;
+    *out = ws;
+    return BLOOMHIP_OK;
+}
+
+bool probe_partitioned(const bloomhip_filter *f, int owner_strategy, size_t n) {
+    const bool able = f->mp.fast && ((f->m + (1ull << kSegBits) - 1) >> kSegBits) <= kPartMaxBins;
+    if (!able) return false;
+    const int st = f->probe_strategy != BLOOMHIP_PROBE_AUTO ? f->probe_strategy : owner_strategy;
+    if (st == BLOOMHIP_PROBE_PARTITION) return true;
+    if (st == BLOOMHIP_PROBE_GATHER) return false;
+    // AUTO: gathers while the filter stays in each XCD's L2; beyond that the
+    // MALL's random-line rate caps gathers and the partitioned probe wins
+    // (DESIGN.md §5).
+    return (f->m + 7) / 8 > kProbeGatherMaxBytes && n >= kProbePartitionMinKeys;
+}
+
 int run_partition(bloomhip_filter *f, const KeySpan &ks, hipStream_t s) {
-    const size_t nbins = (size_t)((f->m + (1ull << kSegBits) - 1) >> kSegBits);
-    // Expected positions per full segment, plus a wide margin: bins that
-    // still fill up spill into global atomics (exact, just slower).
-    const double expect = 3.0 * (double)ks.n * (double)(1ull << kSegBits) / (double)f->m;
-    size_t cap = (size_t)(expect + 8.0 * std::sqrt(expect) + 1024.0);
-    cap = std::min<size_t>((cap + 3) & ~(size_t)3, 3 * ks.n + 4);
-    cap = (cap + 3) & ~(size_t)3;
-    if (cap > 0xFFFFFFF0ull) return BLOOMHIP_ERANGE;
-    HIP_TRY(grow(reinterpret_cast<void **>(&f->d_bins), &f->bins_bytes, nbins * cap * 4));
-    if (!f->d_counts) HIP_TRY(hipMalloc(&f->d_counts, kPartMaxBins * 4));
-    PartitionWorkspace ws{f->d_bins, f->d_counts, cap, nbins};
-    hipError_t e = timed(f, SLOT_COUNTS, s, [&] {
-        return hipMemsetAsync(f->d_counts, 0, nbins * 4, s);
-    });
-    if (e != hipSuccess) return fail_hip(e, "hipMemsetAsync(counts)");
-    e = timed(f, SLOT_PART_BIN, s, [&] { return launch_part_bin(ks, f->mp, f->d_words, ws, s); });
+    PartitionWorkspace ws{};
+    // Pass 2 wants >= ~1 workgroup per CU; with few segments each segment's
+    // tiles are split over several workgroups that merge with atomicOr.
+    int rc = partition_workspace(f, f->m, ks.n, &ws);
+    if (rc) return rc;
+    hipError_t e = timed(f, SLOT_PART_BIN, s, [&] { return launch_part_bin(ks, f->mp, ws, s); });
     if (e != hipSuccess) return fail_hip(e, "k_part_bin");
     const int merge = f->known_zero ? 0 : 1;
     e = timed(f, SLOT_PART_APPLY, s,
@@ -329,6 +358,7 @@ int bloomhip_destroy(bloomhip_filter *f) {
     if (f->d_out_stage) (void)hipFree(f->d_out_stage);
     if (f->d_bins) (void)hipFree(f->d_bins);
     if (f->d_counts) (void)hipFree(f->d_counts);
+    if (f->d_res) (void)hipFree(f->d_res);
     (void)hipStreamDestroy(f->stream);
     delete f;
     return BLOOMHIP_OK;
@@ -436,16 +466,40 @@ int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const voi
         HIP_TRY(grow(&f0->d_out_stage, &f0->out_stage_bytes, out_bytes));
         dout = reinterpret_cast<uint64_t *>(f0->d_out_stage);
     }
-    for (int j0 = 0; j0 < nf; j0 += kMaxProbeFilters) {
-        ProbeTable t{};
-        t.nf = std::min(nf - j0, kMaxProbeFilters);
-        for (int j = 0; j < t.nf; j++) {
-            t.words[j] = filters[j0 + j]->d_words;
-            t.mp[j] = filters[j0 + j]->mp;
+    // Large filters: partitioned probe, one filter at a time; the rest:
+    // gathers, up to kMaxProbeFilters per launch.
+    std::vector<int> gather_idx;
+    for (int j = 0; j < nf; j++) {
+        if (!probe_partitioned(filters[j], f0->probe_strategy, n)) {
+            gather_idx.push_back(j);
+            continue;
         }
+        PartitionWorkspace ws{};
+        rc = partition_workspace(f0, filters[j]->m, n, &ws);
+        if (rc) return rc;
+        HIP_TRY(grow(reinterpret_cast<void **>(&f0->d_res), &f0->res_bytes, n));
+        hipError_t e = timed(f0, SLOT_PROBE_PART, s, [&] {
+            return launch_probe_partitioned(ks, filters[j]->mp, filters[j]->d_words, ws, f0->d_res,
+                                            dout + (size_t)j * nw, s);
+        });
+        if (e != hipSuccess) return fail_hip(e, "partitioned probe launch");
+    }
+    for (size_t j0 = 0; j0 < gather_idx.size();) {
+        // one launch per run of consecutive output rows (<= kMaxProbeFilters)
+        ProbeTable t{};
+        const int row0 = gather_idx[j0];
+        size_t j1 = j0;
+        while (j1 < gather_idx.size() && j1 - j0 < (size_t)kMaxProbeFilters &&
+               gather_idx[j1] == row0 + (int)(j1 - j0)) {
+            t.words[j1 - j0] = filters[gather_idx[j1]]->d_words;
+            t.mp[j1 - j0] = filters[gather_idx[j1]]->mp;
+            j1++;
+        }
+        t.nf = (int)(j1 - j0);
         hipError_t e = timed(f0, SLOT_PROBE, s,
-                             [&] { return launch_probe(ks, t, dout + (size_t)j0 * nw, nw, s); });
+                             [&] { return launch_probe(ks, t, dout + (size_t)row0 * nw, nw, s); });
         if (e != hipSuccess) return fail_hip(e, "k_probe launch");
+        j0 = j1;
     }
     if (!out_on_device) {
         hipError_t e = timed(f0, SLOT_COPY, s, [&] {
@@ -511,6 +565,15 @@ int bloomhip_set_strategy(bloomhip_filter *f, int strategy) {
     if (strategy != BLOOMHIP_BUILD_AUTO && !strategy_supported(f, strategy)) return BLOOMHIP_EINVAL;
     std::lock_guard<std::mutex> lk(f->mu);
     f->strategy = strategy;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_set_probe_strategy(bloomhip_filter *f, int strategy) {
+    g_last_error.clear();
+    if (!f || strategy < BLOOMHIP_PROBE_AUTO || strategy > BLOOMHIP_PROBE_PARTITION)
+        return BLOOMHIP_EINVAL;
+    std::lock_guard<std::mutex> lk(f->mu);
+    f->probe_strategy = strategy;
     return BLOOMHIP_OK;
 }
 

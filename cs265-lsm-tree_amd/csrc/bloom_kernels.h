@@ -32,19 +32,31 @@ struct ProbeTable {
     int nf;
 };
 
-// LDS bytes a private-bitmap workgroup may use (m/8 must fit).
-constexpr size_t kLdsBitmapBytes = 64 * 1024;
+// LDS bytes a private-bitmap workgroup may use (m/8 must fit): 160 KiB per
+// CU on gfx950, one such workgroup per CU.
+constexpr size_t kLdsBitmapBytes = 160 * 1024;
 
 // Partition build geometry: one LDS segment = 2^kSegBits bits.
 constexpr int kSegBits = 19;  // 64 KiB of bitmap per segment workgroup
-constexpr size_t kPartTileKeys = 4096;
+constexpr uint32_t kSegMask = (1u << kSegBits) - 1u;
+constexpr int kPartBlock = 512;
+constexpr int kPartKPT = 8;  // keys per thread in pass 1
+constexpr size_t kPartTileKeys = (size_t)kPartBlock * kPartKPT;  // 4096
+constexpr int kPartTilePos = (int)kPartTileKeys * 3;
 constexpr size_t kPartMaxBins = 2048;  // m <= 2^30 bits
 
+// Probe: filters up to this size are gathered directly (they stay resident in
+// every XCD's 4 MiB L2); larger ones use the partitioned probe when the batch
+// has at least kProbePartitionMinKeys keys.
+constexpr size_t kProbeGatherMaxBytes = 8u << 20;
+constexpr size_t kProbePartitionMinKeys = 1u << 18;
+
 struct PartitionWorkspace {
-    uint32_t *bins;        // [nbins * cap] segment-local offsets
-    uint32_t *counts;      // [nbins] fill counters
-    size_t cap;            // capacity per bin (entries)
+    uint32_t *pos;         // [ntiles * kPartTilePos] tile-sorted segment offsets
+    uint32_t *run_starts;  // [ntiles * (nbins + 1)]
+    size_t ntiles;
     size_t nbins;
+    size_t nsplit;         // pass-2 workgroups per segment
 };
 
 // Kernels enqueued on `stream`; all return hipSuccess or the launch error.
@@ -52,12 +64,18 @@ hipError_t launch_build_atomic(const KeySpan &keys, const ModParams &mp, uint32_
                                hipStream_t stream);
 hipError_t launch_build_lds(const KeySpan &keys, const ModParams &mp, uint32_t *words,
                             hipStream_t stream);
-hipError_t launch_part_bin(const KeySpan &keys, const ModParams &mp, uint32_t *words,
-                           const PartitionWorkspace &ws, hipStream_t stream);
+hipError_t launch_part_bin(const KeySpan &keys, const ModParams &mp, const PartitionWorkspace &ws,
+                           hipStream_t stream);
 // merge_existing: OR into the current bitmap instead of overwriting segments.
 hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const PartitionWorkspace &ws,
                              int merge_existing, hipStream_t stream);
 hipError_t launch_probe(const KeySpan &keys, const ProbeTable &t, uint64_t *out, size_t nwords_out,
                         hipStream_t stream);
+// Partitioned probe of one filter (fast mod, nbins <= kPartMaxBins): bin the
+// keys' positions by segment, test each segment in LDS, pack the result
+// bytes `res` (n bytes of workspace) into out[ceil(n/64)].
+hipError_t launch_probe_partitioned(const KeySpan &keys, const ModParams &mp, const uint32_t *words,
+                                    const PartitionWorkspace &ws, uint8_t *res, uint64_t *out,
+                                    hipStream_t stream);
 
 }  // namespace bloomhip

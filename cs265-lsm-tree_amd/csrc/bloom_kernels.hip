@@ -12,11 +12,12 @@
 //   lds       — m/8 <= 64 KiB: every workgroup builds a private copy of the
 //               whole filter in LDS with ds_or, then ORs its non-zero words
 //               into the global bitmap.
-//   partition — m <= 2^30: pass 1 hashes a tile of keys, counting-sorts the
-//               3 positions by 2^19-bit segment in LDS and appends each
-//               segment's run to that segment's bin; pass 2 gives every
-//               segment to one workgroup, which ORs its bin into a 64 KiB
-//               LDS image and writes the segment out with coalesced stores.
+//   partition — m <= 2^30: pass 1 hashes a tile of keys and counting-sorts
+//               its 3 positions by 2^19-bit segment in LDS, writing the sorted
+//               tile and its per-segment run starts; pass 2 gives every
+//               segment to one workgroup, which gathers that segment's run
+//               from every tile, ORs it into a 64 KiB LDS image and writes
+//               the segment out with coalesced stores.  No global atomics.
 #include "bloom_kernels.h"
 
 namespace bloomhip {
@@ -114,36 +115,43 @@ __global__ void __launch_bounds__(kBlock) k_build_lds(KeySpan ks, ModParams mp,
 }
 
 // ---------------------------------------------------------------------------
-// partition pass 1: hash a tile, counting-sort its positions by segment in
-// LDS, reserve each segment's run in its bin, write the runs out.
+// partition pass 1 (k_part_bin): one 512-thread workgroup per tile of
+// kPartTileKeys keys.  Each thread hashes kPartKPT keys; the 3 positions are
+// counting-sorted by segment (pos >> kSegBits) in LDS and the sorted tile is
+// written contiguously to pos_out[tile * kPartTilePos ...].  Row `tile` of
+// run_starts holds the exclusive prefix of the tile's per-segment counts
+// (nbins + 1 entries), so segment b's run of this tile is
+// [run_starts[tile][b], run_starts[tile][b+1]).  No global atomics.
 // ---------------------------------------------------------------------------
-constexpr int kMaxBins = 2048;
-constexpr int kTilePos = (int)kPartTileKeys * 3;
-constexpr int kKeysPerThread = (int)kPartTileKeys / kBlock;  // 16
+constexpr int kMaxBins = (int)kPartMaxBins;
+constexpr int kScanPer = (kMaxBins + 1 + kPartBlock - 1) / kPartBlock;  // entries per thread
 
-template <int LAYOUT>
-__global__ void __launch_bounds__(kBlock) k_part_bin(KeySpan ks, ModParams mp,
-                                                     uint32_t *__restrict__ words,
-                                                     PartitionWorkspace ws) {
-    __shared__ uint32_t s_sorted[kTilePos];   // 48 KiB
-    __shared__ uint32_t s_hist[kMaxBins];     // counts, then run starts in s_sorted
-    __shared__ uint32_t s_base[kMaxBins];     // reserved start of the run in the bin
-    __shared__ uint32_t s_wave_sum[kBlock / 64];
+// ABLATE (timing builds only, tools/ubench): 1 = skip the sorted-tile store,
+// 2 = also skip the LDS scatter, 3 = hash only.  The product launches 0.
+// TAG (partitioned probe): each entry also carries its key's index in the
+// tile, (key_in_tile << kSegBits) | offset, and the tile's result bytes
+// res[key] are initialised to 1 ("every test passed so far").
+template <int LAYOUT, int ABLATE = 0, bool TAG = false>
+__global__ void __launch_bounds__(kPartBlock) k_part_bin(KeySpan ks, ModParams mp,
+                                                         uint32_t *__restrict__ pos_out,
+                                                         uint32_t *__restrict__ run_starts,
+                                                         int nbins, uint8_t *__restrict__ res) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_sorted[kPartTilePos];
+    __shared__ uint32_t s_hist[kMaxBins + 1];
+    __shared__ uint32_t s_wsum[kPartBlock / 64];
 
-    const int nbins = (int)ws.nbins;
-    const size_t tile0 = (size_t)blockIdx.x * kPartTileKeys;
     const int tid = threadIdx.x;
-
-    for (int b = tid; b < nbins; b += kBlock) s_hist[b] = 0;
+    const size_t tile = blockIdx.x;
+    const size_t tile0 = tile * kPartTileKeys;
+    for (int b = tid; b <= nbins; b += kPartBlock) s_hist[b] = 0;
     __syncthreads();
 
-    // 1. positions + rank within segment (LDS atomics).
-    uint32_t pos[kKeysPerThread * 3];
-    uint32_t rank[kKeysPerThread * 3];
-    int nvalid = 0;
+    // 1. positions, and each one's rank inside its segment (LDS atomics).
+    uint32_t pos[kPartKPT * 3];
+    uint32_t rank[kPartKPT * 3];
 #pragma unroll
-    for (int j = 0; j < kKeysPerThread; j++) {
-        const size_t i = tile0 + (size_t)j * kBlock + tid;
+    for (int j = 0; j < kPartKPT; j++) {
+        const size_t i = tile0 + (size_t)j * kPartBlock + tid;
         if (i < ks.n) {
             int32_t k;
             if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
@@ -151,27 +159,33 @@ __global__ void __launch_bounds__(kBlock) k_part_bin(KeySpan ks, ModParams mp,
             pos[3 * j + 0] = pos32(raw_hash1(k), mp);
             pos[3 * j + 1] = pos32(raw_hash2(k), mp);
             pos[3 * j + 2] = pos32(raw_hash3(k), mp);
-            nvalid = j + 1;
+            if constexpr (TAG) res[i] = 1;
+            if constexpr (ABLATE < 3) {
+#pragma unroll
+                for (int h = 0; h < 3; h++)
+                    rank[3 * j + h] = atomicAdd(&s_hist[pos[3 * j + h] >> kSegBits], 1u);
+            }
         }
     }
+    if constexpr (ABLATE == 3) {
+        uint32_t acc = 0;
 #pragma unroll
-    for (int j = 0; j < kKeysPerThread * 3; j++) {
-        if (j < nvalid * 3) rank[j] = atomicAdd(&s_hist[pos[j] >> kSegBits], 1u);
+        for (int j = 0; j < kPartKPT * 3; j++) acc ^= pos[j];
+        if (acc == 0x9E3779B9u) pos_out[tid] = acc;
+        return;
     }
     __syncthreads();
 
-    // 2. exclusive scan of the histogram (block-wide) -> run starts; reserve
-    //    each non-empty run in its bin with one global atomic.
-    constexpr int kPer = kMaxBins / kBlock;  // 8 bins per thread
-    uint32_t local[kPer];
+    // 2. exclusive scan of the nbins+1 counts (the extra slot is 0 and
+    //    receives the tile total).
+    uint32_t local[kScanPer];
     uint32_t tsum = 0;
 #pragma unroll
-    for (int q = 0; q < kPer; q++) {
-        const int b = tid * kPer + q;
-        local[q] = b < nbins ? s_hist[b] : 0u;
+    for (int q = 0; q < kScanPer; q++) {
+        const int b = tid * kScanPer + q;
+        local[q] = b <= nbins ? s_hist[b] : 0u;
         tsum += local[q];
     }
-    // wave-level inclusive scan of tsum
     const int lane = tid & 63, wave = tid >> 6;
     uint32_t incl = tsum;
 #pragma unroll
@@ -179,100 +193,178 @@ __global__ void __launch_bounds__(kBlock) k_part_bin(KeySpan ks, ModParams mp,
         const uint32_t o = __shfl_up(incl, off, 64);
         if (lane >= off) incl += o;
     }
-    if (lane == 63) s_wave_sum[wave] = incl;
+    if (lane == 63) s_wsum[wave] = incl;
     __syncthreads();
-    uint32_t wave_off = 0;
-    for (int w = 0; w < wave; w++) wave_off += s_wave_sum[w];
-    uint32_t run = wave_off + incl - tsum;
+    uint32_t run = incl - tsum;
+    for (int w = 0; w < wave; w++) run += s_wsum[w];
+    uint32_t *row = run_starts + tile * (size_t)(nbins + 1);
 #pragma unroll
-    for (int q = 0; q < kPer; q++) {
-        const int b = tid * kPer + q;
-        if (b < nbins) {
-            const uint32_t c = local[q];
-            s_hist[b] = run;  // run start inside s_sorted
-            s_base[b] = c ? atomicAdd(&ws.counts[b], c) : 0u;
-            run += c;
+    for (int q = 0; q < kScanPer; q++) {
+        const int b = tid * kScanPer + q;
+        if (b <= nbins) {
+            s_hist[b] = run;
+            row[b] = run;
+            run += local[q];
         }
     }
     __syncthreads();
 
+    if constexpr (ABLATE >= 2) return;
     // 3. scatter into the LDS image sorted by segment.
 #pragma unroll
-    for (int j = 0; j < kKeysPerThread * 3; j++) {
-        if (j < nvalid * 3) s_sorted[s_hist[pos[j] >> kSegBits] + rank[j]] = pos[j];
+    for (int j = 0; j < kPartKPT; j++) {
+        const size_t i = tile0 + (size_t)j * kPartBlock + tid;
+        if (i < ks.n) {
+#pragma unroll
+            for (int h = 0; h < 3; h++) {
+                const uint32_t p = pos[3 * j + h];
+                uint32_t e = p & kSegMask;
+                if constexpr (TAG) e |= (uint32_t)(j * kPartBlock + tid) << kSegBits;
+                s_sorted[s_hist[p >> kSegBits] + rank[3 * j + h]] = e;
+            }
+        }
     }
     __syncthreads();
 
-    // 4. copy runs out: consecutive threads take consecutive sorted entries,
-    //    so each wave writes one or two contiguous runs.
+    if constexpr (ABLATE >= 1) {
+        if (s_sorted[tid] == 0xFFFFFFFFu) pos_out[tid] = 0;
+        return;
+    }
+    // 4. the sorted tile goes out with 16-byte stores.
     const size_t tile_keys = min((size_t)kPartTileKeys, ks.n - tile0);
     const int npos = (int)tile_keys * 3;
-    const uint32_t segmask = (1u << kSegBits) - 1u;
-    for (int e = tid; e < npos; e += kBlock) {
-        const uint32_t p = s_sorted[e];
-        const uint32_t b = p >> kSegBits;
-        const uint32_t dst = s_base[b] + (uint32_t)e - s_hist[b];
-        if (dst < ws.cap) {
-            ws.bins[(size_t)b * ws.cap + dst] = p & segmask;
-        } else {
-            // bin full (only for adversarial key sets): set the bit directly.
-            __hip_atomic_fetch_or(words + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    uint32_t *dst = pos_out + tile * (size_t)kPartTilePos;
+    const int nq = npos / 4;
+    for (int q = tid; q < nq; q += kPartBlock)
+        reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(s_sorted)[q];
+    for (int e = nq * 4 + tid; e < npos; e += kPartBlock) dst[e] = s_sorted[e];
 }
 
 // ---------------------------------------------------------------------------
-// partition pass 2: one workgroup per 2^19-bit segment.
+// partition pass 2 (k_part_apply): workgroup (b, split) ORs segment b's runs
+// of tiles [split*tps, (split+1)*tps) into a 64 KiB LDS image, then writes the
+// segment (nsplit == 1: plain 16-B stores, OR-merged with the old bitmap when
+// it may be non-zero; nsplit > 1: atomicOr of the non-zero words).
 // ---------------------------------------------------------------------------
 constexpr int kSegWords = (1 << kSegBits) / 32;  // 16384 u32 = 64 KiB
+constexpr int kApplyBlock = 1024;
+constexpr int kApplyWaves = kApplyBlock / 64;
+constexpr int kApplyChunk = kApplyBlock;  // tiles whose run bounds are staged in LDS at once
+constexpr int kApplyBatch = 8;            // runs per batch; two batches in flight
+static_assert(kApplyChunk == kApplyWaves * 64, "one 64-tile slice per wave per chunk");
+static_assert(kPartTileKeys <= (1u << (32 - kSegBits)), "probe tags must fit beside the offset");
 
-__global__ void __launch_bounds__(1024) k_part_apply(uint32_t *__restrict__ words, uint64_t nw32,
-                                                     PartitionWorkspace ws, int merge_existing) {
+// PROBE = false: build (OR every entry into the zeroed LDS image, write the
+// segment).  PROBE = true: the LDS image is the filter's segment; an entry
+// whose bit is clear zeroes its key's result byte (any failed test fails the
+// key, so concurrent stores of 0 from different workgroups agree).
+template <bool PROBE>
+__global__ void __launch_bounds__(kApplyBlock) k_part_apply(
+    const uint32_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
+    int nbins, int nsplit, uint32_t *__restrict__ words, uint64_t nw32, int merge_existing,
+    uint8_t *__restrict__ res) {
     extern __shared__ __attribute__((aligned(16))) uint32_t seg[];
-    const uint32_t b = blockIdx.x;
-    for (int i = threadIdx.x; i < kSegWords; i += blockDim.x) seg[i] = 0;
-    __syncthreads();
+    __shared__ uint2 s_run[kApplyChunk];  // (start, end) of this segment's run per tile
+    const int b = (int)(blockIdx.x % (unsigned)nbins);
+    const int split = (int)(blockIdx.x / (unsigned)nbins);
+    const int tps = (ntiles + nsplit - 1) / nsplit;
+    const int t_begin = split * tps;
+    const int t_end = min(ntiles, t_begin + tps);
+    if constexpr (PROBE) {
+        const uint64_t w0 = (uint64_t)b * kSegWords;
+        const int nseg = (int)(min(nw32, w0 + kSegWords) - w0);
+        for (int i = threadIdx.x; i < kSegWords; i += kApplyBlock)
+            seg[i] = i < nseg ? words[w0 + i] : 0u;
+    } else {
+        for (int i = threadIdx.x; i < kSegWords / 4; i += kApplyBlock)
+            reinterpret_cast<uint4 *>(seg)[i] = make_uint4(0, 0, 0, 0);
+    }
 
-    const uint32_t total = ws.counts[b];
-    const uint32_t cnt = min((uint32_t)ws.cap, total);
-    // A full bin spilled positions straight into this segment with atomics.
-    const bool merge = merge_existing || total > (uint32_t)ws.cap;
-    const uint32_t *src = ws.bins + (size_t)b * ws.cap;
-    const uint32_t nq = cnt / 4;
-    const uint4 *src4 = reinterpret_cast<const uint4 *>(src);  // cap is a multiple of 4
-    for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
-        const uint4 v = src4[q];
-        atomicOr(&seg[v.x >> 5], 1u << (v.x & 31));
-        atomicOr(&seg[v.y >> 5], 1u << (v.y & 31));
-        atomicOr(&seg[v.z >> 5], 1u << (v.z & 31));
-        atomicOr(&seg[v.w >> 5], 1u << (v.w & 31));
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const size_t stride = (size_t)nbins + 1;
+    // Run bounds of tile t for segment b, fetched one chunk ahead.
+    auto fetch_run = [&](int t) -> uint2 {
+        if (t >= t_end) return make_uint2(0, 0);
+        const uint32_t *row = run_starts + (size_t)t * stride + b;
+        return make_uint2(row[0], row[1]);
+    };
+    uint2 r_next = fetch_run(t_begin + (int)threadIdx.x);
+    for (int c0 = t_begin; c0 < t_end; c0 += kApplyChunk) {
+        __syncthreads();  // previous chunk's s_run fully consumed (and seg zeroed)
+        s_run[threadIdx.x] = r_next;
+        __syncthreads();
+        r_next = fetch_run(c0 + kApplyChunk + (int)threadIdx.x);
+        // wave w owns tiles c0 + 64w .. c0 + 64w + 63 of this chunk; its runs
+        // are read kApplyBatch at a time, the next batch's loads issued before
+        // the current batch's LDS ORs.
+        const int wt0 = wave * 64;
+        const int wtn = max(0, min(64, t_end - (c0 + wt0)));
+        const uint32_t *wbase = pos + (size_t)(c0 + wt0) * kPartTilePos;
+        uint32_t cur[kApplyBatch], nxt[kApplyBatch];
+        auto load_batch = [&](int k0, uint32_t (&v)[kApplyBatch]) {
+#pragma unroll
+            for (int k = 0; k < kApplyBatch; k++) {
+                const uint2 r = k0 + k < wtn ? s_run[wt0 + k0 + k] : make_uint2(0, 0);
+                const uint32_t e = r.x + lane;
+                v[k] = e < r.y ? wbase[(size_t)(k0 + k) * kPartTilePos + e] : 0xFFFFFFFFu;
+            }
+        };
+        auto apply_one = [&](uint32_t v, int k) {
+            if constexpr (PROBE) {
+                const uint32_t off = v & kSegMask;
+                if (!((seg[off >> 5] >> (off & 31)) & 1u))
+                    res[(size_t)(c0 + wt0 + k) * kPartTileKeys + (v >> kSegBits)] = 0;
+            } else {
+                atomicOr(&seg[v >> 5], 1u << (v & 31));
+            }
+        };
+        auto or_batch = [&](const uint32_t (&v)[kApplyBatch], int k0) {
+#pragma unroll
+            for (int k = 0; k < kApplyBatch; k++)
+                if (v[k] != 0xFFFFFFFFu) apply_one(v[k], k0 + k);
+        };
+        if (wtn > 0) load_batch(0, cur);
+        for (int k0 = 0; k0 < wtn; k0 += kApplyBatch) {
+            if (k0 + kApplyBatch < wtn) load_batch(k0 + kApplyBatch, nxt);
+            or_batch(cur, k0);
+#pragma unroll
+            for (int k = 0; k < kApplyBatch; k++) cur[k] = nxt[k];
+        }
+        // entries past the first 64 of a run (only when segments are few)
+        for (int k = 0; k < wtn; k++) {
+            const uint2 r = s_run[wt0 + k];
+            for (uint32_t e = r.x + 64 + lane; e < r.y; e += 64)
+                apply_one(wbase[(size_t)k * kPartTilePos + e], k);
+        }
     }
-    for (uint32_t e = nq * 4 + threadIdx.x; e < cnt; e += blockDim.x) {
-        const uint32_t v = src[e];
-        atomicOr(&seg[v >> 5], 1u << (v & 31));
-    }
+    if constexpr (PROBE) return;
     __syncthreads();
 
     const uint64_t w0 = (uint64_t)b * kSegWords;
     const uint64_t wend = min(nw32, w0 + kSegWords);
     const int nseg = (int)(wend - w0);
     uint32_t *dst = words + w0;
-    if (nseg == kSegWords) {
+    if (nsplit > 1) {
+        for (int i = threadIdx.x; i < nseg; i += kApplyBlock) {
+            const uint32_t w = seg[i];
+            if (w) __hip_atomic_fetch_or(dst + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else if (nseg == kSegWords) {
         uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
         const uint4 *seg4 = reinterpret_cast<const uint4 *>(seg);
-        for (int q = threadIdx.x; q < kSegWords / 4; q += blockDim.x) {
+        for (int q = threadIdx.x; q < kSegWords / 4; q += kApplyBlock) {
             uint4 v = seg4[q];
-            if (merge) {
+            if (merge_existing) {
                 const uint4 o = dst4[q];
                 v.x |= o.x; v.y |= o.y; v.z |= o.z; v.w |= o.w;
             }
             dst4[q] = v;
         }
     } else {
-        for (int i = threadIdx.x; i < nseg; i += blockDim.x) {
+        for (int i = threadIdx.x; i < nseg; i += kApplyBlock) {
             uint32_t v = seg[i];
-            if (merge) v |= dst[i];
+            if (merge_existing) v |= dst[i];
             dst[i] = v;
         }
     }
@@ -286,6 +378,8 @@ __global__ void __launch_bounds__(1024) k_part_apply(uint32_t *__restrict__ word
 __device__ __forceinline__ bool test_bit(const uint32_t *w, uint64_t p) {
     return (w[p >> 5] >> (p & 31)) & 1u;
 }
+
+constexpr int kProbeGroup = 4;  // filters whose gathers a lane has in flight together
 
 template <int LAYOUT>
 __global__ void __launch_bounds__(kBlock) k_probe(KeySpan ks, ProbeTable t,
@@ -301,23 +395,51 @@ __global__ void __launch_bounds__(kBlock) k_probe(KeySpan ks, ProbeTable t,
             if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
             else k = load_key(ks, i);
         }
-        const uint64_t h1 = raw_hash1(k), h2 = raw_hash2(k), h3 = raw_hash3(k);
-        for (int f = 0; f < t.nf; f++) {
-            const ModParams &mp = t.mp[f];
-            const uint32_t *fw = t.words[f];
-            bool hit = false;
-            if (valid) {
-                if (mp.fast) {
-                    hit = test_bit(fw, pos32(h1, mp)) && test_bit(fw, pos32(h2, mp)) &&
-                          test_bit(fw, pos32(h3, mp));
-                } else {
-                    hit = test_bit(fw, h1 % mp.m) && test_bit(fw, h2 % mp.m) &&
-                          test_bit(fw, h3 % mp.m);
+        const uint64_t h[3] = {raw_hash1(k), raw_hash2(k), raw_hash3(k)};
+        for (int g = 0; g < t.nf; g += kProbeGroup) {
+            // Round r tests hash r of every still-alive (key, filter) pair of
+            // the group: the reference's short-circuit && per filter, with the
+            // group's gathers of one round in flight together.
+            bool alive[kProbeGroup];
+#pragma unroll
+            for (int q = 0; q < kProbeGroup; q++) alive[q] = valid && g + q < t.nf;
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                uint32_t word[kProbeGroup], bit[kProbeGroup];
+#pragma unroll
+                for (int q = 0; q < kProbeGroup; q++) {
+                    if (alive[q]) {
+                        const ModParams &mp = t.mp[g + q];
+                        const uint64_t p = mod_any(h[r], mp);
+                        word[q] = t.words[g + q][p >> 5];
+                        bit[q] = (uint32_t)p & 31u;
+                    }
                 }
+#pragma unroll
+                for (int q = 0; q < kProbeGroup; q++)
+                    if (alive[q]) alive[q] = (word[q] >> bit[q]) & 1u;
             }
-            const uint64_t ballot = __ballot(hit);
-            if (lane == 0) out[(size_t)f * nw_out + w] = ballot;
+#pragma unroll
+            for (int q = 0; q < kProbeGroup; q++) {
+                const uint64_t ballot = __ballot(alive[q]);
+                if (lane == 0 && g + q < t.nf) out[(size_t)(g + q) * nw_out + w] = ballot;
+            }
         }
+    }
+}
+
+// Partitioned probe, last step: result bytes -> packed bits (one u64 per
+// 64 keys).
+__global__ void __launch_bounds__(kBlock) k_probe_pack(const uint8_t *__restrict__ res, size_t n,
+                                                       uint64_t *__restrict__ out, size_t nw_out) {
+    const int lane = threadIdx.x & 63;
+    const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    for (size_t w = wave; w < nw_out; w += nwaves) {
+        const size_t i = w * 64 + lane;
+        const bool hit = i < n && res[i] != 0;
+        const uint64_t ballot = __ballot(hit);
+        if (lane == 0) out[w] = ballot;
     }
 }
 
@@ -351,15 +473,25 @@ hipError_t launch_build_lds(const KeySpan &ks, const ModParams &mp, uint32_t *wo
                             hipStream_t stream) {
     if (ks.n == 0) return hipSuccess;
     const uint32_t nw32 = (uint32_t)((mp.m + 31) / 32);
-    const size_t lds = (size_t)nw32 * 4;
-    // Enough keys per block that the merge (nw32 words) stays a small share.
-    size_t kpb = (size_t)nw32 * 2;
-    if (kpb < 4096) kpb = 4096;
+    const size_t lds = ((size_t)nw32 * 4 + 15) & ~(size_t)15;
+    if (lds > kLdsBitmapBytes) return hipErrorInvalidValue;
+    // Keys per block: enough that the merge (nw32 atomics) stays a small
+    // share, few enough that the grid covers the chip.
+    size_t kpb = (size_t)nw32 / 4;
+    if (kpb < 2048) kpb = 2048;
     unsigned grid = (unsigned)((ks.n + kpb - 1) / kpb);
     if (grid > 1024) {
         grid = 1024;
         kpb = (ks.n + grid - 1) / grid;
     }
+    static const bool attr_set = [] {  // > 64 KiB of dynamic LDS must be opted into
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_build_lds<KEYS_PACKED>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBitmapBytes);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_build_lds<KEYS_STRIDED>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBitmapBytes);
+        return true;
+    }();
+    (void)attr_set;
     if (ks.layout == KEYS_PACKED)
         k_build_lds<KEYS_PACKED><<<grid, kBlock, lds, stream>>>(ks, mp, words, nw32, kpb);
     else
@@ -367,22 +499,52 @@ hipError_t launch_build_lds(const KeySpan &ks, const ModParams &mp, uint32_t *wo
     return hipGetLastError();
 }
 
-hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, uint32_t *words,
-                           const PartitionWorkspace &ws, hipStream_t stream) {
+hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                           hipStream_t stream) {
     if (ks.n == 0) return hipSuccess;
-    const unsigned grid = (unsigned)((ks.n + kPartTileKeys - 1) / kPartTileKeys);
+    const unsigned grid = (unsigned)ws.ntiles;
     if (ks.layout == KEYS_PACKED)
-        k_part_bin<KEYS_PACKED><<<grid, kBlock, 0, stream>>>(ks, mp, words, ws);
+        k_part_bin<KEYS_PACKED><<<grid, kPartBlock, 0, stream>>>(ks, mp, ws.pos, ws.run_starts,
+                                                                 (int)ws.nbins, nullptr);
     else
-        k_part_bin<KEYS_STRIDED><<<grid, kBlock, 0, stream>>>(ks, mp, words, ws);
+        k_part_bin<KEYS_STRIDED><<<grid, kPartBlock, 0, stream>>>(ks, mp, ws.pos, ws.run_starts,
+                                                                  (int)ws.nbins, nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const PartitionWorkspace &ws,
                              int merge_existing, hipStream_t stream) {
+    if (ws.ntiles == 0) return hipSuccess;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
-    k_part_apply<<<(unsigned)ws.nbins, 1024, kSegWords * 4, stream>>>(words, nw32, ws,
-                                                                    merge_existing);
+    const unsigned grid = (unsigned)(ws.nbins * ws.nsplit);
+    k_part_apply<false><<<grid, kApplyBlock, kSegWords * 4, stream>>>(
+        ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit, words, nw32,
+        merge_existing, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, const uint32_t *words,
+                                    const PartitionWorkspace &ws, uint8_t *res, uint64_t *out,
+                                    hipStream_t stream) {
+    if (ks.n == 0) return hipSuccess;
+    const unsigned g1 = (unsigned)ws.ntiles;
+    if (ks.layout == KEYS_PACKED)
+        k_part_bin<KEYS_PACKED, 0, true><<<g1, kPartBlock, 0, stream>>>(
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, res);
+    else
+        k_part_bin<KEYS_STRIDED, 0, true><<<g1, kPartBlock, 0, stream>>>(
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, res);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
+    const unsigned g2 = (unsigned)(ws.nbins * ws.nsplit);
+    k_part_apply<true><<<g2, kApplyBlock, kSegWords * 4, stream>>>(
+        ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit,
+        const_cast<uint32_t *>(words), nw32, 0, res);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t nw = (ks.n + 63) / 64;
+    k_probe_pack<<<grid_for(nw, kBlock / 64, 16384), kBlock, 0, stream>>>(res, ks.n, out, nw);
     return hipGetLastError();
 }
 

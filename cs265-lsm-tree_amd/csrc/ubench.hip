@@ -6,7 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "bloom_math.h"
+#include "bloom_kernels.hip"  // the product kernels, for ablation timing builds
 
 using namespace bloomhip;
 
@@ -99,6 +99,24 @@ extern "C" int ubench_run(int which, void *dbuf, size_t bytes, uint64_t m, int g
         case 4: ub_hash<<<grid, block, 0, s>>>(make_mod_params(m), iters, sink); break;
         case 5: ub_rawhash<<<grid, block, 0, s>>>(iters, sink); break;
         case 6: ub_stream<<<grid, block, 0, s>>>(reinterpret_cast<const uint4 *>(dbuf), bytes / 16 - 1, sink); break;
+        default: return -22;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Pass 1 of the partition build with phases removed (ABLATE 0..3).
+extern "C" int ubench_part_bin(int ablate, const void *keys, size_t n, uint64_t m, uint32_t *pos,
+                               uint32_t *run_starts, void *stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
+    const ModParams mp = make_mod_params(m);
+    const int nbins = (int)((m + (1ull << kSegBits) - 1) >> kSegBits);
+    const unsigned grid = (unsigned)((n + kPartTileKeys - 1) / kPartTileKeys);
+    switch (ablate) {
+        case 0: k_part_bin<KEYS_PACKED, 0><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nullptr); break;
+        case 1: k_part_bin<KEYS_PACKED, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nullptr); break;
+        case 2: k_part_bin<KEYS_PACKED, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nullptr); break;
+        case 3: k_part_bin<KEYS_PACKED, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nullptr); break;
         default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -60,6 +60,11 @@ extern "C" {
 #define BLOOMHIP_BUILD_LDS 2       /* private LDS bitmap per workgroup (m/8 <= LDS) */
 #define BLOOMHIP_BUILD_PARTITION 3 /* hash+bin pass, then LDS segment pass */
 
+/* Probe strategies for bloomhip_test_batch (bloomhip_set_probe_strategy). */
+#define BLOOMHIP_PROBE_AUTO 0      /* gather for L2-sized filters, else partition */
+#define BLOOMHIP_PROBE_GATHER 1    /* per-key gathers of the 3 bits */
+#define BLOOMHIP_PROBE_PARTITION 2 /* bin positions by segment, test in LDS */
+
 typedef struct bloomhip_filter bloomhip_filter;
 
 int bloomhip_abi_version(void);
@@ -120,6 +125,9 @@ int bloomhip_sync(const bloomhip_filter *f, void *stream);
 
 /* Build strategy override (BLOOMHIP_BUILD_*); AUTO by default. */
 int bloomhip_set_strategy(bloomhip_filter *f, int strategy);
+/* Probe strategy (BLOOMHIP_PROBE_*) for this filter; AUTO by default.  In a
+ * test_batch the first filter's setting applies to filters left on AUTO. */
+int bloomhip_set_probe_strategy(bloomhip_filter *f, int strategy);
 /* Strategy AUTO resolved for a batch of n keys on this filter. */
 int bloomhip_resolve_strategy(const bloomhip_filter *f, size_t n, int *strategy_out);
 

@@ -172,10 +172,15 @@ def test_clear_resets():
 
 
 # ---------------------------------------------------------------- probe ----
+PROBES = [bh.PROBE_GATHER, bh.PROBE_PARTITION]
+
+
 @pytest.mark.parametrize("m", [1, 64, 65, 1000, 655_360, 1_000_003, 167_772_160, 2**32 + 15])
-def test_probe_matches_oracle(coracle, m):
+@pytest.mark.parametrize("probe", PROBES, ids=["gather", "partition"])
+def test_probe_matches_oracle(coracle, m, probe):
     keys = rand_keys(100_000 if m < 2**32 else 20_000, 21)
     f = bh.BloomFilter(m)
+    f.set_probe_strategy(probe)   # partition falls back to gathers where it cannot apply
     f.set_batch(keys)
     probe = np.concatenate([keys[:30_000], rand_keys(70_001, 22)])
     got = bh.test_batch([f], probe)[0]
@@ -184,12 +189,15 @@ def test_probe_matches_oracle(coracle, m):
 
 
 def test_probe_many_filters_chunks_past_16(coracle):
+    """20 filters, mixed strategies: gathered ones go out in launches of <= 16
+    consecutive rows around the partitioned ones."""
     rng = np.random.default_rng(3)
     filters, refs = [], []
     for j in range(20):
-        m = int(rng.integers(1000, 3_000_000))
+        m = int(rng.integers(1000, 30_000_000))
         keys = rand_keys(20_000, 100 + j)
         f = bh.BloomFilter(m)
+        f.set_probe_strategy(bh.PROBE_PARTITION if j in (3, 11, 12) else bh.PROBE_GATHER)
         f.set_batch(keys)
         filters.append(f)
         refs.append((m, coracle.build(m, keys)))
@@ -200,11 +208,13 @@ def test_probe_many_filters_chunks_past_16(coracle):
         assert (got[j] == coracle.test(w, m, probe)).all(), j
 
 
-def test_probe_device_buffers_and_strides(coracle, torch_cuda):
+@pytest.mark.parametrize("probe", PROBES, ids=["gather", "partition"])
+def test_probe_device_buffers_and_strides(coracle, torch_cuda, probe):
     torch = torch_cuda
     m = 2_000_003
     keys = rand_keys(64 * 1000 + 37, 31)
     f = bh.BloomFilter(m)
+    f.set_probe_strategy(probe)
     f.set_batch(keys)
     ref = coracle.test(coracle.build(m, keys), m, keys)
     dk = torch.from_numpy(keys).cuda()
@@ -239,12 +249,14 @@ def test_c2_full_bitmap(golden):
         assert int(np.unpackbits(w.view(np.uint8)).sum()) == golden["reference"]["c2_popcount"]
 
 
-def test_c3_probe_five_levels(golden):
+@pytest.mark.parametrize("probe", [bh.PROBE_AUTO] + PROBES, ids=["auto", "gather", "partition"])
+def test_c3_probe_five_levels(golden, probe):
     from bloomhip import workloads as W
     gets, levels = W.c3()
     filters = []
     for lvl, keys, m in levels:
         f = bh.BloomFilter(m)
+        f.set_probe_strategy(probe)
         f.set_batch(keys)
         lv = golden["oracle"]["c3"]["levels"][lvl]
         assert sha(f.words()) == lv["sha256"], lvl

@@ -15,6 +15,9 @@ LIB = ctypes.CDLL(os.path.join(ROOT, "cs265-lsm-tree_amd", "lib", "libbloomhip_u
 LIB.ubench_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 LIB.ubench_run.restype = ctypes.c_int
+LIB.ubench_part_bin.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
+                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+LIB.ubench_part_bin.restype = ctypes.c_int
 
 
 def timeit(which, buf, nbytes, m, grid, block, iters, reps=5):
@@ -31,8 +34,38 @@ def timeit(which, buf, nbytes, m, grid, block, iters, reps=5):
     return a.elapsed_time(b) / reps
 
 
+def part_ablation():
+    """Pass 1 of the partition build on C2 with phases removed."""
+    sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
+    import bloomhip as bh
+    keys = torch.from_numpy(bh.gen_puts(13141, 16_777_216)).cuda()
+    m = 167_772_160
+    ntiles = (keys.numel() + 4095) // 4096
+    nbins = (m + (1 << 19) - 1) >> 19
+    pos = torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda")
+    rs = torch.empty(ntiles * (nbins + 1), dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    names = {0: "full", 1: "no tile store", 2: "no scatter/store", 3: "hash only"}
+    for ab in range(4):
+        for _ in range(3):
+            LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(),
+                                rs.data_ptr(), s.cuda_stream)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(10):
+            LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(),
+                                rs.data_ptr(), s.cuda_stream)
+        b.record(s)
+        torch.cuda.synchronize()
+        print(json.dumps({"op": "k_part_bin", "ablate": names[ab],
+                          "us": round(a.elapsed_time(b) / 10 * 1e3, 2)}), flush=True)
+
+
 def main():
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "part":
+        return part_ablation()
     grid, block = 2048, 256
     threads = grid * block
     out = []
