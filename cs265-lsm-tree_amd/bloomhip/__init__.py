@@ -52,7 +52,7 @@ EXPORTED_SYMBOLS = (
     "bloomhip_clear", "bloomhip_set_batch", "bloomhip_test_batch", "bloomhip_set",
     "bloomhip_is_set", "bloomhip_download", "bloomhip_upload", "bloomhip_sync",
     "bloomhip_set_strategy", "bloomhip_set_probe_strategy", "bloomhip_resolve_strategy", "bloomhip_profile_enable",
-    "bloomhip_profile_read", "bloomhip_profile_reset", "bloomhip_host_positions",
+    "bloomhip_profile_read", "bloomhip_profile_reset", "bloomhip_trim", "bloomhip_host_positions",
     "bloomhip_gen_mt19937", "bloomhip_gen_glibc_rand", "bloomhip_gen_puts",
     "bloomhip_gen_workload",
 )
@@ -117,6 +117,7 @@ def _lib():
             "bloomhip_profile_read": (I, [P, I, ctypes.POINTER(ctypes.c_char_p), PU64,
                                           ctypes.POINTER(ctypes.c_double)]),
             "bloomhip_profile_reset": (I, [P]),
+            "bloomhip_trim": (I, []),
             "bloomhip_host_positions": (I, [U64, P, SZ, P]),
             "bloomhip_gen_mt19937": (I, [ctypes.c_uint32, SZ, P]),
             "bloomhip_gen_glibc_rand": (I, [ctypes.c_uint32, SZ, P]),

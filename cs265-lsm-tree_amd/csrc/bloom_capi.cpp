@@ -12,8 +12,11 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/bloomhip.h"
@@ -94,12 +97,6 @@ struct bloomhip_filter {
     size_t stage_bytes = 0;
     void *d_out_stage = nullptr;
     size_t out_stage_bytes = 0;
-    uint32_t *d_bins = nullptr;    // partition: tile-sorted positions
-    size_t bins_bytes = 0;
-    uint32_t *d_counts = nullptr;  // partition: per-tile run starts
-    size_t counts_bytes = 0;
-    uint8_t *d_res = nullptr;      // partitioned probe: per-key result bytes
-    size_t res_bytes = 0;
 
     bool prof = false;
     uint64_t prof_launches[BLOOMHIP_PROF_SLOTS] = {};
@@ -110,8 +107,11 @@ struct bloomhip_filter {
 
 namespace {
 
-hipStream_t pick_stream(const bloomhip_filter *f, void *stream) {
-    return stream ? reinterpret_cast<hipStream_t>(stream) : f->stream;
+// NULL is HIP's default (null) stream, as everywhere in HIP: work given no
+// stream is ordered with the caller's other default-stream work (e.g. a torch
+// copy on its default stream).
+hipStream_t pick_stream(const bloomhip_filter *, void *stream) {
+    return reinterpret_cast<hipStream_t>(stream);
 }
 
 hipError_t grow(void **ptr, size_t *have, size_t need) {
@@ -126,6 +126,41 @@ hipError_t grow(void **ptr, size_t *have, size_t need) {
     hipError_t e = hipMalloc(ptr, sz);
     if (e == hipSuccess) *have = sz;
     return e;
+}
+
+// Grows *ptr to >= need bytes; a fresh allocation is written once on `s` so
+// its pages are mapped before a kernel's first touch (a first build on fresh
+// 200 MB of workspace otherwise ran 100x slower).
+hipError_t grow_touched(void **ptr, size_t *have, size_t need, hipStream_t s) {
+    if (*have >= need) return hipSuccess;
+    hipError_t e = grow(ptr, have, need);
+    if (e == hipSuccess) e = hipMemsetAsync(*ptr, 0, *have, s);
+    return e;
+}
+
+// Scratch of the partition build / partitioned probe.  Shared by every handle
+// that runs on the same (device, stream): work on one stream is ordered, so
+// one set of buffers serves all of it, allocated (and first touched) once.
+struct Workspace {
+    std::mutex mu;  // held while work using the buffers is enqueued
+    uint32_t *pos = nullptr;  // tile-sorted segment offsets
+    size_t pos_bytes = 0;
+    uint32_t *runs = nullptr;  // per-tile run starts
+    size_t runs_bytes = 0;
+    uint8_t *res = nullptr;  // partitioned probe: result byte per sorted entry
+    size_t res_bytes = 0;
+    uint16_t *slots = nullptr;  // partitioned probe: sorted slot per (key, hash)
+    size_t slots_bytes = 0;
+};
+
+std::mutex g_ws_mu;
+std::map<std::pair<int, hipStream_t>, std::unique_ptr<Workspace>> g_ws;
+
+Workspace *workspace_for(int device, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    auto &w = g_ws[{device, s}];
+    if (!w) w.reset(new Workspace());
+    return w.get();
 }
 
 hipEvent_t take_event(bloomhip_filter *f) {
@@ -223,20 +258,25 @@ int strategy_supported(const bloomhip_filter *f, int strategy) {
     }
 }
 
-// Sizes the partition workspace of `owner` for n keys against filter size m.
-int partition_workspace(bloomhip_filter *owner, uint64_t m, size_t n, PartitionWorkspace *out) {
+// Geometry of a partition pass over n keys for filter size m, with the
+// position/run buffers of `w` grown to fit.
+int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
+                        PartitionWorkspace *out) {
     PartitionWorkspace ws{};
     ws.nbins = (size_t)((m + (1ull << kSegBits) - 1) >> kSegBits);
     ws.ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
-    size_t nsplit = ws.nbins >= 128 ? 1 : (256 + ws.nbins - 1) / ws.nbins;
-    nsplit = std::min(nsplit, std::max<size_t>(1, ws.ntiles / 8));
+    // Pass 2 wants >= ~2 workgroups per CU.  With few segments, each
+    // segment's tiles are split over several workgroups, merged by atomicOr
+    // of their LDS images (cheap next to the positions they read).
+    size_t nsplit = ws.nbins >= 256 ? 1 : (512 + ws.nbins - 1) / ws.nbins;
+    nsplit = std::min(nsplit, ws.ntiles);
     ws.nsplit = std::max<size_t>(1, nsplit);
-    HIP_TRY(grow(reinterpret_cast<void **>(&owner->d_bins), &owner->bins_bytes,
-                 ws.ntiles * (size_t)kPartTilePos * 4));
-    HIP_TRY(grow(reinterpret_cast<void **>(&owner->d_counts), &owner->counts_bytes,
-                 ws.ntiles * (ws.nbins + 1) * 4));
-    ws.pos = owner->d_bins;
-    ws.run_starts = owner->d_counts;
+    HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->pos), &w->pos_bytes,
+                         ws.ntiles * (size_t)kPartTilePos * 4, s));
+    HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->runs), &w->runs_bytes,
+                         ws.ntiles * (ws.nbins + 1) * 4, s));
+    ws.pos = w->pos;
+    ws.run_starts = w->runs;
     *out = ws;
     return BLOOMHIP_OK;
 }
@@ -254,10 +294,10 @@ bool probe_partitioned(const bloomhip_filter *f, int owner_strategy, size_t n) {
 }
 
 int run_partition(bloomhip_filter *f, const KeySpan &ks, hipStream_t s) {
+    Workspace *w = workspace_for(f->device, s);
+    std::lock_guard<std::mutex> lk(w->mu);
     PartitionWorkspace ws{};
-    // Pass 2 wants >= ~1 workgroup per CU; with few segments each segment's
-    // tiles are split over several workgroups that merge with atomicOr.
-    int rc = partition_workspace(f, f->m, ks.n, &ws);
+    int rc = partition_workspace(w, f->m, ks.n, s, &ws);
     if (rc) return rc;
     hipError_t e = timed(f, SLOT_PART_BIN, s, [&] { return launch_part_bin(ks, f->mp, ws, s); });
     if (e != hipSuccess) return fail_hip(e, "k_part_bin");
@@ -356,9 +396,6 @@ int bloomhip_destroy(bloomhip_filter *f) {
     if (f->d_words) (void)hipFree(f->d_words);
     if (f->d_stage) (void)hipFree(f->d_stage);
     if (f->d_out_stage) (void)hipFree(f->d_out_stage);
-    if (f->d_bins) (void)hipFree(f->d_bins);
-    if (f->d_counts) (void)hipFree(f->d_counts);
-    if (f->d_res) (void)hipFree(f->d_res);
     (void)hipStreamDestroy(f->stream);
     delete f;
     return BLOOMHIP_OK;
@@ -474,13 +511,18 @@ int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const voi
             gather_idx.push_back(j);
             continue;
         }
+        Workspace *w = workspace_for(f0->device, s);
+        std::lock_guard<std::mutex> wl(w->mu);
         PartitionWorkspace ws{};
-        rc = partition_workspace(f0, filters[j]->m, n, &ws);
+        rc = partition_workspace(w, filters[j]->m, n, s, &ws);
         if (rc) return rc;
-        HIP_TRY(grow(reinterpret_cast<void **>(&f0->d_res), &f0->res_bytes, n));
+        HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->res), &w->res_bytes,
+                             ws.ntiles * (size_t)kPartTilePos, s));
+        HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->slots), &w->slots_bytes,
+                             ws.ntiles * 3 * kPartTileKeys * sizeof(uint16_t), s));
         hipError_t e = timed(f0, SLOT_PROBE_PART, s, [&] {
-            return launch_probe_partitioned(ks, filters[j]->mp, filters[j]->d_words, ws, f0->d_res,
-                                            dout + (size_t)j * nw, s);
+            return launch_probe_partitioned(ks, filters[j]->mp, filters[j]->d_words, ws, w->res,
+                                            w->slots, dout + (size_t)j * nw, s);
         });
         if (e != hipSuccess) return fail_hip(e, "partitioned probe launch");
     }
@@ -616,6 +658,21 @@ int bloomhip_profile_reset(bloomhip_filter *f) {
         f->prof_launches[i] = 0;
     }
     return rc;
+}
+
+int bloomhip_trim(void) {
+    g_last_error.clear();
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (auto &kv : g_ws) {
+        Workspace *w = kv.second.get();
+        std::lock_guard<std::mutex> wl(w->mu);
+        DeviceGuard g(kv.first.first);
+        (void)hipStreamSynchronize(kv.first.second);
+        for (void *p : {(void *)w->pos, (void *)w->runs, (void *)w->res, (void *)w->slots})
+            if (p) (void)hipFree(p);
+    }
+    g_ws.clear();
+    return BLOOMHIP_OK;
 }
 
 int bloomhip_host_positions(uint64_t m, const int32_t *keys, size_t n, uint64_t *out) {

@@ -48,7 +48,7 @@ constexpr size_t kPartMaxBins = 2048;  // m <= 2^30 bits
 // Probe: filters up to this size are gathered directly (they stay resident in
 // every XCD's 4 MiB L2); larger ones use the partitioned probe when the batch
 // has at least kProbePartitionMinKeys keys.
-constexpr size_t kProbeGatherMaxBytes = 8u << 20;
+constexpr size_t kProbeGatherMaxBytes = 2u << 20;
 constexpr size_t kProbePartitionMinKeys = 1u << 18;
 
 struct PartitionWorkspace {
@@ -72,10 +72,12 @@ hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const Partiti
 hipError_t launch_probe(const KeySpan &keys, const ProbeTable &t, uint64_t *out, size_t nwords_out,
                         hipStream_t stream);
 // Partitioned probe of one filter (fast mod, nbins <= kPartMaxBins): bin the
-// keys' positions by segment, test each segment in LDS, pack the result
-// bytes `res` (n bytes of workspace) into out[ceil(n/64)].
+// keys' positions by segment (recording each position's sorted slot), test
+// each segment in LDS writing one result byte per sorted entry, then AND each
+// key's three bytes into out[ceil(n/64)].  Workspace: res holds
+// ntiles*kPartTilePos bytes, slots ntiles*3*kPartTileKeys u16.
 hipError_t launch_probe_partitioned(const KeySpan &keys, const ModParams &mp, const uint32_t *words,
-                                    const PartitionWorkspace &ws, uint8_t *res, uint64_t *out,
-                                    hipStream_t stream);
+                                    const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
+                                    uint64_t *out, hipStream_t stream);
 
 }  // namespace bloomhip

@@ -115,129 +115,162 @@ __global__ void __launch_bounds__(kBlock) k_build_lds(KeySpan ks, ModParams mp,
 }
 
 // ---------------------------------------------------------------------------
-// partition pass 1 (k_part_bin): one 512-thread workgroup per tile of
-// kPartTileKeys keys.  Each thread hashes kPartKPT keys; the 3 positions are
-// counting-sorted by segment (pos >> kSegBits) in LDS and the sorted tile is
-// written contiguously to pos_out[tile * kPartTilePos ...].  Row `tile` of
-// run_starts holds the exclusive prefix of the tile's per-segment counts
-// (nbins + 1 entries), so segment b's run of this tile is
+// partition pass 1 (k_part_bin): persistent 512-thread workgroups walk tiles
+// of kPartTileKeys keys.  Each thread hashes kPartKPT keys; the 3 positions
+// are counting-sorted by segment (pos >> kSegBits) in LDS and the sorted tile
+// (segment offsets) is written contiguously to pos_out[tile*kPartTilePos..].
+// Row `tile` of run_starts holds the exclusive prefix of the tile's
+// per-segment counts (nbins + 1 entries), so segment b's run of this tile is
 // [run_starts[tile][b], run_starts[tile][b+1]).  No global atomics.
+//
+// The next tile's keys are loaded while the current tile is sorted, and the
+// workgroup barriers wait only for LDS (lgkmcnt), so the sorted tile's
+// stores drain under the next tile's hashing.
+//
+// SLOTS (partitioned probe): also write, per key and hash, the index its
+// position got in the sorted tile: slots[(tile*3 + h)*kPartTileKeys + key].
 // ---------------------------------------------------------------------------
 constexpr int kMaxBins = (int)kPartMaxBins;
 constexpr int kScanPer = (kMaxBins + 1 + kPartBlock - 1) / kPartBlock;  // entries per thread
 
+// Workgroup barrier that waits for this wave's LDS operations only.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ void load_tile_keys(const KeySpan &ks, size_t tile, int tid,
+                                               int32_t (&k)[kPartKPT]) {
+    const size_t tile0 = tile * kPartTileKeys;
+#pragma unroll
+    for (int j = 0; j < kPartKPT; j++) {
+        const size_t i = tile0 + (size_t)j * kPartBlock + tid;
+        if (i < ks.n) {
+            if constexpr (LAYOUT == KEYS_PACKED) k[j] = reinterpret_cast<const int32_t *>(ks.base)[i];
+            else k[j] = load_key(ks, i);
+        } else {
+            k[j] = 0;
+        }
+    }
+}
+
 // ABLATE (timing builds only, tools/ubench): 1 = skip the sorted-tile store,
 // 2 = also skip the LDS scatter, 3 = hash only.  The product launches 0.
-// TAG (partitioned probe): each entry also carries its key's index in the
-// tile, (key_in_tile << kSegBits) | offset, and the tile's result bytes
-// res[key] are initialised to 1 ("every test passed so far").
-template <int LAYOUT, int ABLATE = 0, bool TAG = false>
-__global__ void __launch_bounds__(kPartBlock) k_part_bin(KeySpan ks, ModParams mp,
+template <int LAYOUT, int ABLATE = 0, bool SLOTS = false>
+__global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParams mp,
                                                          uint32_t *__restrict__ pos_out,
                                                          uint32_t *__restrict__ run_starts,
-                                                         int nbins, uint8_t *__restrict__ res) {
+                                                         int nbins, size_t ntiles,
+                                                         uint16_t *__restrict__ slots) {
     __shared__ __attribute__((aligned(16))) uint32_t s_sorted[kPartTilePos];
     __shared__ uint32_t s_hist[kMaxBins + 1];
     __shared__ uint32_t s_wsum[kPartBlock / 64];
 
     const int tid = threadIdx.x;
-    const size_t tile = blockIdx.x;
-    const size_t tile0 = tile * kPartTileKeys;
-    for (int b = tid; b <= nbins; b += kPartBlock) s_hist[b] = 0;
-    __syncthreads();
-
-    // 1. positions, and each one's rank inside its segment (LDS atomics).
-    uint32_t pos[kPartKPT * 3];
-    uint32_t rank[kPartKPT * 3];
-#pragma unroll
-    for (int j = 0; j < kPartKPT; j++) {
-        const size_t i = tile0 + (size_t)j * kPartBlock + tid;
-        if (i < ks.n) {
-            int32_t k;
-            if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
-            else k = load_key(ks, i);
-            pos[3 * j + 0] = pos32(raw_hash1(k), mp);
-            pos[3 * j + 1] = pos32(raw_hash2(k), mp);
-            pos[3 * j + 2] = pos32(raw_hash3(k), mp);
-            if constexpr (TAG) res[i] = 1;
-            if constexpr (ABLATE < 3) {
-#pragma unroll
-                for (int h = 0; h < 3; h++)
-                    rank[3 * j + h] = atomicAdd(&s_hist[pos[3 * j + h] >> kSegBits], 1u);
-            }
-        }
-    }
-    if constexpr (ABLATE == 3) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int j = 0; j < kPartKPT * 3; j++) acc ^= pos[j];
-        if (acc == 0x9E3779B9u) pos_out[tid] = acc;
-        return;
-    }
-    __syncthreads();
-
-    // 2. exclusive scan of the nbins+1 counts (the extra slot is 0 and
-    //    receives the tile total).
-    uint32_t local[kScanPer];
-    uint32_t tsum = 0;
-#pragma unroll
-    for (int q = 0; q < kScanPer; q++) {
-        const int b = tid * kScanPer + q;
-        local[q] = b <= nbins ? s_hist[b] : 0u;
-        tsum += local[q];
-    }
     const int lane = tid & 63, wave = tid >> 6;
-    uint32_t incl = tsum;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += o;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    __syncthreads();
-    uint32_t run = incl - tsum;
-    for (int w = 0; w < wave; w++) run += s_wsum[w];
-    uint32_t *row = run_starts + tile * (size_t)(nbins + 1);
-#pragma unroll
-    for (int q = 0; q < kScanPer; q++) {
-        const int b = tid * kScanPer + q;
-        if (b <= nbins) {
-            s_hist[b] = run;
-            row[b] = run;
-            run += local[q];
-        }
-    }
-    __syncthreads();
+    int32_t kcur[kPartKPT], knext[kPartKPT];
+    if (blockIdx.x < ntiles) load_tile_keys<LAYOUT>(ks, blockIdx.x, tid, kcur);
 
-    if constexpr (ABLATE >= 2) return;
-    // 3. scatter into the LDS image sorted by segment.
+    for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const size_t tile0 = tile * kPartTileKeys;
+        const int tile_keys = (int)min((size_t)kPartTileKeys, ks.n - tile0);
+        for (int b = tid; b <= nbins; b += kPartBlock) s_hist[b] = 0;
+        lds_barrier();  // also: the previous tile's s_sorted reads are done
+        if (tile + gridDim.x < ntiles) load_tile_keys<LAYOUT>(ks, tile + gridDim.x, tid, knext);
+
+        // 1. positions, and each one's rank inside its segment (LDS atomics).
+        uint32_t pos[kPartKPT * 3];
+        uint32_t rank[kPartKPT * 3];
 #pragma unroll
-    for (int j = 0; j < kPartKPT; j++) {
-        const size_t i = tile0 + (size_t)j * kPartBlock + tid;
-        if (i < ks.n) {
+        for (int j = 0; j < kPartKPT; j++) {
+            if (j * kPartBlock + tid < tile_keys) {
+                const int32_t k = kcur[j];
+                pos[3 * j + 0] = pos32(raw_hash1(k), mp);
+                pos[3 * j + 1] = pos32(raw_hash2(k), mp);
+                pos[3 * j + 2] = pos32(raw_hash3(k), mp);
+                if constexpr (ABLATE < 3) {
 #pragma unroll
-            for (int h = 0; h < 3; h++) {
-                const uint32_t p = pos[3 * j + h];
-                uint32_t e = p & kSegMask;
-                if constexpr (TAG) e |= (uint32_t)(j * kPartBlock + tid) << kSegBits;
-                s_sorted[s_hist[p >> kSegBits] + rank[3 * j + h]] = e;
+                    for (int h = 0; h < 3; h++)
+                        rank[3 * j + h] = atomicAdd(&s_hist[pos[3 * j + h] >> kSegBits], 1u);
+                }
             }
         }
-    }
-    __syncthreads();
+        if constexpr (ABLATE == 3) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < kPartKPT * 3; j++) acc ^= pos[j];
+            if (acc == 0x9E3779B9u) pos_out[tid] = acc;
+#pragma unroll
+            for (int j = 0; j < kPartKPT; j++) kcur[j] = knext[j];
+            continue;
+        }
+        lds_barrier();
 
-    if constexpr (ABLATE >= 1) {
-        if (s_sorted[tid] == 0xFFFFFFFFu) pos_out[tid] = 0;
-        return;
+        // 2. exclusive scan of the nbins+1 counts (the extra slot is 0 and
+        //    receives the tile total).
+        uint32_t local[kScanPer];
+        uint32_t tsum = 0;
+#pragma unroll
+        for (int q = 0; q < kScanPer; q++) {
+            const int b = tid * kScanPer + q;
+            local[q] = b <= nbins ? s_hist[b] : 0u;
+            tsum += local[q];
+        }
+        uint32_t incl = tsum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+        }
+        if (lane == 63) s_wsum[wave] = incl;
+        lds_barrier();
+        uint32_t run = incl - tsum;
+        for (int w = 0; w < wave; w++) run += s_wsum[w];
+        uint32_t *row = run_starts + tile * (size_t)(nbins + 1);
+#pragma unroll
+        for (int q = 0; q < kScanPer; q++) {
+            const int b = tid * kScanPer + q;
+            if (b <= nbins) {
+                s_hist[b] = run;
+                row[b] = run;
+                run += local[q];
+            }
+        }
+        lds_barrier();
+
+        if constexpr (ABLATE < 2) {
+            // 3. scatter into the LDS image sorted by segment.
+#pragma unroll
+            for (int j = 0; j < kPartKPT; j++) {
+                if (j * kPartBlock + tid < tile_keys) {
+#pragma unroll
+                    for (int h = 0; h < 3; h++) {
+                        const uint32_t p = pos[3 * j + h];
+                        const uint32_t slot = s_hist[p >> kSegBits] + rank[3 * j + h];
+                        s_sorted[slot] = p & kSegMask;
+                        if constexpr (SLOTS)
+                            slots[(tile * 3 + h) * kPartTileKeys + j * kPartBlock + tid] =
+                                (uint16_t)slot;
+                    }
+                }
+            }
+            lds_barrier();
+        }
+
+        if constexpr (ABLATE == 0) {
+            // 4. the sorted tile goes out with 16-byte stores.
+            const int npos = tile_keys * 3;
+            uint32_t *dst = pos_out + tile * (size_t)kPartTilePos;
+            const int nq = npos / 4;
+            for (int q = tid; q < nq; q += kPartBlock)
+                reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(s_sorted)[q];
+            for (int e = nq * 4 + tid; e < npos; e += kPartBlock) dst[e] = s_sorted[e];
+        } else if constexpr (ABLATE == 1) {
+            if (s_sorted[tid] == 0xFFFFFFFFu) pos_out[tid] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < kPartKPT; j++) kcur[j] = knext[j];
     }
-    // 4. the sorted tile goes out with 16-byte stores.
-    const size_t tile_keys = min((size_t)kPartTileKeys, ks.n - tile0);
-    const int npos = (int)tile_keys * 3;
-    uint32_t *dst = pos_out + tile * (size_t)kPartTilePos;
-    const int nq = npos / 4;
-    for (int q = tid; q < nq; q += kPartBlock)
-        reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(s_sorted)[q];
-    for (int e = nq * 4 + tid; e < npos; e += kPartBlock) dst[e] = s_sorted[e];
 }
 
 // ---------------------------------------------------------------------------
@@ -247,26 +280,49 @@ __global__ void __launch_bounds__(kPartBlock) k_part_bin(KeySpan ks, ModParams m
 // it may be non-zero; nsplit > 1: atomicOr of the non-zero words).
 // ---------------------------------------------------------------------------
 constexpr int kSegWords = (1 << kSegBits) / 32;  // 16384 u32 = 64 KiB
+
+// Bijective block -> work-unit map that gives each XCD a contiguous range of
+// units (cdna_hip_programming.md §5.5 T1, bijective form for n % 8 != 0).
+__device__ __forceinline__ unsigned xcd_remap(unsigned x, unsigned n) {
+    constexpr unsigned kXcds = 8;
+    const unsigned q = n / kXcds, r = n % kXcds;
+    const unsigned xcd = x % kXcds, idx = x / kXcds;
+    // XCD xcd owns units [start, start + q + (xcd < r)).
+    const unsigned start = xcd * q + min(xcd, r);
+    return start + idx;
+}
 constexpr int kApplyBlock = 1024;
 constexpr int kApplyWaves = kApplyBlock / 64;
 constexpr int kApplyChunk = kApplyBlock;  // tiles whose run bounds are staged in LDS at once
-constexpr int kApplyBatch = 8;            // runs per batch; two batches in flight
+constexpr int kApplyBatch = 16;           // runs per batch; two batches in flight
+// At >= this many segments a tile's runs average <= 48 entries (12288/256).
+constexpr size_t kShortRunBins = 256;
 static_assert(kApplyChunk == kApplyWaves * 64, "one 64-tile slice per wave per chunk");
 static_assert(kPartTileKeys <= (1u << (32 - kSegBits)), "probe tags must fit beside the offset");
 
 // PROBE = false: build (OR every entry into the zeroed LDS image, write the
-// segment).  PROBE = true: the LDS image is the filter's segment; an entry
-// whose bit is clear zeroes its key's result byte (any failed test fails the
-// key, so concurrent stores of 0 from different workgroups agree).
-template <bool PROBE>
+// segment).  PROBE = true: the LDS image is the filter's segment; each entry's
+// bit is written as one result byte at the entry's own index in the sorted
+// tile (res[tile*kPartTilePos + index]), so the result stores follow the runs
+// and coalesce like the loads.
+// LONG_RUNS: few segments, so runs span several 64-entry steps; the wave
+// walks (batch, offset) steps.  Otherwise runs rarely exceed 64 entries: one
+// step per batch, and the rare longer run finishes in a per-tile tail loop.
+template <bool PROBE, bool LONG_RUNS>
 __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
     const uint32_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, int nsplit, uint32_t *__restrict__ words, uint64_t nw32, int merge_existing,
     uint8_t *__restrict__ res) {
     extern __shared__ __attribute__((aligned(16))) uint32_t seg[];
     __shared__ uint2 s_run[kApplyChunk];  // (start, end) of this segment's run per tile
-    const int b = (int)(blockIdx.x % (unsigned)nbins);
-    const int split = (int)(blockIdx.x / (unsigned)nbins);
+    // Neighbouring segments' runs share 128-B lines of every sorted tile, so
+    // give consecutive segments to workgroups on one XCD (blocks are dealt
+    // round-robin over the 8 XCDs): block x -> unit (x % 8) * per + x / 8.
+    // A bijection on [0, nunits); placement only affects speed.
+    const unsigned nunits = (unsigned)(nbins * nsplit);
+    const unsigned unit = xcd_remap(blockIdx.x, nunits);
+    const int b = (int)(unit % (unsigned)nbins);
+    const int split = (int)(unit / (unsigned)nbins);
     const int tps = (ntiles + nsplit - 1) / nsplit;
     const int t_begin = split * tps;
     const int t_end = min(ntiles, t_begin + tps);
@@ -301,41 +357,87 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
         const int wt0 = wave * 64;
         const int wtn = max(0, min(64, t_end - (c0 + wt0)));
         const uint32_t *wbase = pos + (size_t)(c0 + wt0) * kPartTilePos;
+        // The wave's work is a sequence of steps (k0, off): entries
+        // [off, off + 64) of the runs of tiles k0 .. k0 + kApplyBatch - 1.
+        // Loads of the next step are issued before the current step's LDS
+        // work, so two steps (2 * kApplyBatch loads per lane) are in flight.
         uint32_t cur[kApplyBatch], nxt[kApplyBatch];
-        auto load_batch = [&](int k0, uint32_t (&v)[kApplyBatch]) {
+        auto batch_maxlen = [&](int k0) -> uint32_t {
+            uint32_t ml = 0;
+#pragma unroll
+            for (int k = 0; k < kApplyBatch; k++) {
+                if (k0 + k < wtn) {
+                    const uint2 r = s_run[wt0 + k0 + k];
+                    ml = max(ml, r.y - r.x);
+                }
+            }
+            return __builtin_amdgcn_readfirstlane(ml);
+        };
+        auto load_step = [&](int k0, uint32_t off, uint32_t (&v)[kApplyBatch]) {
 #pragma unroll
             for (int k = 0; k < kApplyBatch; k++) {
                 const uint2 r = k0 + k < wtn ? s_run[wt0 + k0 + k] : make_uint2(0, 0);
-                const uint32_t e = r.x + lane;
+                const uint32_t e = r.x + off + lane;
                 v[k] = e < r.y ? wbase[(size_t)(k0 + k) * kPartTilePos + e] : 0xFFFFFFFFu;
             }
         };
-        auto apply_one = [&](uint32_t v, int k) {
-            if constexpr (PROBE) {
-                const uint32_t off = v & kSegMask;
-                if (!((seg[off >> 5] >> (off & 31)) & 1u))
-                    res[(size_t)(c0 + wt0 + k) * kPartTileKeys + (v >> kSegBits)] = 0;
-            } else {
-                atomicOr(&seg[v >> 5], 1u << (v & 31));
+        auto apply_step = [&](int k0, uint32_t off, const uint32_t (&v)[kApplyBatch]) {
+#pragma unroll
+            for (int k = 0; k < kApplyBatch; k++) {
+                if (v[k] == 0xFFFFFFFFu) continue;
+                if constexpr (PROBE) {
+                    const uint32_t e = s_run[wt0 + k0 + k].x + off + lane;
+                    res[(size_t)(c0 + wt0 + k0 + k) * kPartTilePos + e] =
+                        (seg[v[k] >> 5] >> (v[k] & 31)) & 1u;
+                } else {
+                    (void)off;
+                    atomicOr(&seg[v[k] >> 5], 1u << (v[k] & 31));
+                }
             }
         };
-        auto or_batch = [&](const uint32_t (&v)[kApplyBatch], int k0) {
+        if (wtn <= 0) continue;
+        if constexpr (LONG_RUNS) {
+            int k0 = 0;
+            uint32_t off = 0, ml = batch_maxlen(0);
+            load_step(k0, off, cur);
+            while (true) {
+                int nk0 = k0;
+                uint32_t noff = off + 64, nml = ml;
+                if (noff >= ml) {
+                    nk0 = k0 + kApplyBatch;
+                    noff = 0;
+                    nml = nk0 < wtn ? batch_maxlen(nk0) : 0;
+                }
+                const bool more = nk0 < wtn;
+                if (more) load_step(nk0, noff, nxt);
+                apply_step(k0, off, cur);
+                if (!more) break;
 #pragma unroll
-            for (int k = 0; k < kApplyBatch; k++)
-                if (v[k] != 0xFFFFFFFFu) apply_one(v[k], k0 + k);
-        };
-        if (wtn > 0) load_batch(0, cur);
-        for (int k0 = 0; k0 < wtn; k0 += kApplyBatch) {
-            if (k0 + kApplyBatch < wtn) load_batch(k0 + kApplyBatch, nxt);
-            or_batch(cur, k0);
+                for (int k = 0; k < kApplyBatch; k++) cur[k] = nxt[k];
+                k0 = nk0;
+                off = noff;
+                ml = nml;
+            }
+        } else {
+            load_step(0, 0, cur);
+            for (int k0 = 0; k0 < wtn; k0 += kApplyBatch) {
+                if (k0 + kApplyBatch < wtn) load_step(k0 + kApplyBatch, 0, nxt);
+                apply_step(k0, 0, cur);
 #pragma unroll
-            for (int k = 0; k < kApplyBatch; k++) cur[k] = nxt[k];
-        }
-        // entries past the first 64 of a run (only when segments are few)
-        for (int k = 0; k < wtn; k++) {
-            const uint2 r = s_run[wt0 + k];
-            for (uint32_t e = r.x + 64 + lane; e < r.y; e += 64)
-                apply_one(wbase[(size_t)k * kPartTilePos + e], k);
+                for (int k = 0; k < kApplyBatch; k++) cur[k] = nxt[k];
+            }
+            for (int k = 0; k < wtn; k++) {  // entries past the first 64 of a run
+                const uint2 r = s_run[wt0 + k];
+                for (uint32_t e = r.x + 64 + lane; e < r.y; e += 64) {
+                    const uint32_t v = wbase[(size_t)k * kPartTilePos + e];
+                    if constexpr (PROBE) {
+                        res[(size_t)(c0 + wt0 + k) * kPartTilePos + e] =
+                            (seg[v >> 5] >> (v & 31)) & 1u;
+                    } else {
+                        atomicOr(&seg[v >> 5], 1u << (v & 31));
+                    }
+                }
+            }
         }
     }
     if constexpr (PROBE) return;
@@ -375,10 +477,6 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
 // modulo each filter's m; per filter the AND of the three bit tests (with the
 // reference's short-circuit) is packed with a 64-lane ballot into one u64.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool test_bit(const uint32_t *w, uint64_t p) {
-    return (w[p >> 5] >> (p & 31)) & 1u;
-}
-
 constexpr int kProbeGroup = 4;  // filters whose gathers a lane has in flight together
 
 template <int LAYOUT>
@@ -428,19 +526,50 @@ __global__ void __launch_bounds__(kBlock) k_probe(KeySpan ks, ProbeTable t,
     }
 }
 
-// Partitioned probe, last step: result bytes -> packed bits (one u64 per
-// 64 keys).
-__global__ void __launch_bounds__(kBlock) k_probe_pack(const uint8_t *__restrict__ res, size_t n,
-                                                       uint64_t *__restrict__ out, size_t nw_out) {
-    const int lane = threadIdx.x & 63;
-    const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
-    for (size_t w = wave; w < nw_out; w += nwaves) {
-        const size_t i = w * 64 + lane;
-        const bool hit = i < n && res[i] != 0;
+// Partitioned probe, last step (k_probe_combine): one workgroup per tile
+// stages the tile's result bytes (sorted order) in LDS and, for each key,
+// ANDs the bytes at its three slots; a 64-lane ballot packs 64 keys per u64.
+constexpr int kCombineBlock = 256;
+
+__global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
+    const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, size_t n,
+    uint64_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_r[kPartTilePos];
+    const size_t tile = blockIdx.x;
+    const size_t tile0 = tile * kPartTileKeys;
+    const int tile_keys = (int)min((size_t)kPartTileKeys, n - tile0);
+    const uint4 *src = reinterpret_cast<const uint4 *>(res + tile * (size_t)kPartTilePos);
+    for (int q = threadIdx.x; q < kPartTilePos / 16; q += kCombineBlock)
+        reinterpret_cast<uint4 *>(s_r)[q] = src[q];
+    __syncthreads();
+    const uint16_t *sl = slots + tile * 3 * kPartTileKeys;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int j = 0; j < (int)kPartTileKeys / kCombineBlock; j++) {
+        const int key = j * kCombineBlock + (int)threadIdx.x;
+        bool hit = false;
+        if (key < tile_keys)
+            hit = s_r[sl[key]] & s_r[sl[kPartTileKeys + key]] & s_r[sl[2 * kPartTileKeys + key]];
         const uint64_t ballot = __ballot(hit);
-        if (lane == 0) out[w] = ballot;
+        const int base = j * kCombineBlock + wave * 64;
+        if (lane == 0 && base < tile_keys) out[(tile0 + base) / 64] = ballot;
     }
+}
+
+// Persistent pass-1 grid: two 57-KiB-LDS workgroups per CU.
+inline unsigned part_bin_grid(size_t ntiles) {
+    static int cus[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (cus[dev] == 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            c <= 0)
+            c = 256;
+        cus[dev] = c;
+    }
+    const size_t g = (size_t)cus[dev] * 2;
+    return (unsigned)(ntiles < g ? ntiles : g);
 }
 
 inline unsigned grid_for(size_t work_items, unsigned per_block, unsigned cap) {
@@ -502,13 +631,13 @@ hipError_t launch_build_lds(const KeySpan &ks, const ModParams &mp, uint32_t *wo
 hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                            hipStream_t stream) {
     if (ks.n == 0) return hipSuccess;
-    const unsigned grid = (unsigned)ws.ntiles;
+    const unsigned grid = part_bin_grid(ws.ntiles);
     if (ks.layout == KEYS_PACKED)
-        k_part_bin<KEYS_PACKED><<<grid, kPartBlock, 0, stream>>>(ks, mp, ws.pos, ws.run_starts,
-                                                                 (int)ws.nbins, nullptr);
+        k_part_bin<KEYS_PACKED><<<grid, kPartBlock, 0, stream>>>(
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, ws.ntiles, nullptr);
     else
-        k_part_bin<KEYS_STRIDED><<<grid, kPartBlock, 0, stream>>>(ks, mp, ws.pos, ws.run_starts,
-                                                                  (int)ws.nbins, nullptr);
+        k_part_bin<KEYS_STRIDED><<<grid, kPartBlock, 0, stream>>>(
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, ws.ntiles, nullptr);
     return hipGetLastError();
 }
 
@@ -517,34 +646,43 @@ hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const Partiti
     if (ws.ntiles == 0) return hipSuccess;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
     const unsigned grid = (unsigned)(ws.nbins * ws.nsplit);
-    k_part_apply<false><<<grid, kApplyBlock, kSegWords * 4, stream>>>(
-        ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit, words, nw32,
-        merge_existing, nullptr);
+    if (ws.nbins >= kShortRunBins)
+        k_part_apply<false, false><<<grid, kApplyBlock, kSegWords * 4, stream>>>(
+            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit, words, nw32,
+            merge_existing, nullptr);
+    else
+        k_part_apply<false, true><<<grid, kApplyBlock, kSegWords * 4, stream>>>(
+            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit, words, nw32,
+            merge_existing, nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, const uint32_t *words,
-                                    const PartitionWorkspace &ws, uint8_t *res, uint64_t *out,
-                                    hipStream_t stream) {
+                                    const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
+                                    uint64_t *out, hipStream_t stream) {
     if (ks.n == 0) return hipSuccess;
-    const unsigned g1 = (unsigned)ws.ntiles;
+    const unsigned g1 = part_bin_grid(ws.ntiles);
     if (ks.layout == KEYS_PACKED)
         k_part_bin<KEYS_PACKED, 0, true><<<g1, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, res);
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, ws.ntiles, slots);
     else
         k_part_bin<KEYS_STRIDED, 0, true><<<g1, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, res);
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, ws.ntiles, slots);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
     const unsigned g2 = (unsigned)(ws.nbins * ws.nsplit);
-    k_part_apply<true><<<g2, kApplyBlock, kSegWords * 4, stream>>>(
-        ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit,
-        const_cast<uint32_t *>(words), nw32, 0, res);
+    if (ws.nbins >= kShortRunBins)
+        k_part_apply<true, false><<<g2, kApplyBlock, kSegWords * 4, stream>>>(
+            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit,
+            const_cast<uint32_t *>(words), nw32, 0, res);
+    else
+        k_part_apply<true, true><<<g2, kApplyBlock, kSegWords * 4, stream>>>(
+            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit,
+            const_cast<uint32_t *>(words), nw32, 0, res);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const size_t nw = (ks.n + 63) / 64;
-    k_probe_pack<<<grid_for(nw, kBlock / 64, 16384), kBlock, 0, stream>>>(res, ks.n, out, nw);
+    k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out);
     return hipGetLastError();
 }
 

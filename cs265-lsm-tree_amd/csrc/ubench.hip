@@ -111,12 +111,13 @@ extern "C" int ubench_part_bin(int ablate, const void *keys, size_t n, uint64_t 
     const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
     const ModParams mp = make_mod_params(m);
     const int nbins = (int)((m + (1ull << kSegBits) - 1) >> kSegBits);
-    const unsigned grid = (unsigned)((n + kPartTileKeys - 1) / kPartTileKeys);
+    const size_t ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
+    const unsigned grid = part_bin_grid(ntiles);
     switch (ablate) {
-        case 0: k_part_bin<KEYS_PACKED, 0><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nullptr); break;
-        case 1: k_part_bin<KEYS_PACKED, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nullptr); break;
-        case 2: k_part_bin<KEYS_PACKED, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nullptr); break;
-        case 3: k_part_bin<KEYS_PACKED, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nullptr); break;
+        case 0: k_part_bin<KEYS_PACKED, 0><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, ntiles, nullptr); break;
+        case 1: k_part_bin<KEYS_PACKED, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, ntiles, nullptr); break;
+        case 2: k_part_bin<KEYS_PACKED, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, ntiles, nullptr); break;
+        case 3: k_part_bin<KEYS_PACKED, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, ntiles, nullptr); break;
         default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;

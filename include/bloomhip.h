@@ -19,8 +19,9 @@
  * is_set booleans.  k = 3 with the reference's three fixed hashes.
  *
  * Conventions
- *   - Plain C types only; `void *stream` is a hipStream_t (NULL = the filter's
- *     own stream).  No HIP or torch headers are needed to bind this ABI.
+ *   - Plain C types only; `void *stream` is a hipStream_t, NULL meaning HIP's
+ *     default (null) stream as in every HIP API.  No HIP or torch headers are
+ *     needed to bind this ABI.
  *   - Every entry point returns an int status: 0 on success, a negative
  *     errno-style code on failure; nothing throws across the ABI.  The
  *     reference has no error path at all (m == 0 is a SIGFPE there,
@@ -89,7 +90,8 @@ int bloomhip_device(const bloomhip_filter *f, int *device_out);
 /* Device address of the bitmap (ceil(m/64) uint64 blocks), for zero-copy
  * interop.  Valid until bloomhip_destroy. */
 int bloomhip_device_words(const bloomhip_filter *f, void **dptr_out);
-/* The handle's own stream (used when a call is given stream = NULL). */
+/* A non-blocking stream owned by the handle, for callers that want the
+ * filter's work off the default stream (pass it as `stream`). */
 int bloomhip_stream(const bloomhip_filter *f, void **stream_out);
 
 /* Reset every bit to 0. */
@@ -120,7 +122,7 @@ int bloomhip_is_set(const bloomhip_filter *f, int32_t key, int *hit_out);
 int bloomhip_download(const bloomhip_filter *f, uint64_t *words, size_t nwords, void *stream);
 int bloomhip_upload(bloomhip_filter *f, const uint64_t *words, size_t nwords, void *stream);
 
-/* Wait for all work queued on `stream` (NULL: the filter's stream). */
+/* Wait for all work queued on `stream` (NULL: the default stream). */
 int bloomhip_sync(const bloomhip_filter *f, void *stream);
 
 /* Build strategy override (BLOOMHIP_BUILD_*); AUTO by default. */
@@ -140,6 +142,10 @@ int bloomhip_profile_enable(bloomhip_filter *f, int enable);
 int bloomhip_profile_read(bloomhip_filter *f, int slot, const char **name_out,
                           uint64_t *launches_out, double *ms_out);
 int bloomhip_profile_reset(bloomhip_filter *f);
+
+/* Free the scratch the partition build / partitioned probe cache per
+ * (device, stream).  Waits for those streams; call when no build is queued. */
+int bloomhip_trim(void);
 
 /* Self-test hook (no GPU needed): the engine's own position arithmetic —
  * the same inline functions the kernels run — evaluated on the host.
