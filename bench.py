@@ -154,6 +154,7 @@ def main():
     import torch
 
     import bloomhip as bh
+    from bloomhip import shard
     from bloomhip import workloads as W
 
     torch.cuda.set_device(local)
@@ -211,9 +212,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = shard.max_over_ranks(elapsed, dist, device="cuda")
 
     # Per-kernel device time: the same K steps again with every launch
     # bracketed by HIP events on the launch stream (kept out of the timed
@@ -228,9 +227,7 @@ def main():
     f.profile(False)
 
     if dist:
-        ok = torch.tensor([0 if verified is False else 1], dtype=torch.int32, device="cuda")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        all_ok = bool(ok.item())
+        all_ok = shard.all_ranks_ok(verified is not False, dist, device="cuda")
     else:
         all_ok = verified is not False
 
