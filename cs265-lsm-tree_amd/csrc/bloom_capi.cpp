@@ -235,6 +235,11 @@ int device_keys(bloomhip_filter *f, const void *keys, size_t n, size_t stride, i
     return BLOOMHIP_OK;
 }
 
+bool partition_able(const bloomhip_filter *f) {
+    PartitionWorkspace ws{};
+    return f->mp.fast && plan_segments(f->m, device_cu_count(), &ws);
+}
+
 int resolve_strategy(const bloomhip_filter *f, size_t n) {
     if (f->strategy != BLOOMHIP_BUILD_AUTO) return f->strategy;
     if (!f->mp.fast) return BLOOMHIP_BUILD_ATOMIC;
@@ -243,8 +248,9 @@ int resolve_strategy(const bloomhip_filter *f, size_t n) {
         // Worth a private LDS copy once the batch outweighs the merge.
         return n >= (size_t)(f->m / 64) ? BLOOMHIP_BUILD_LDS : BLOOMHIP_BUILD_ATOMIC;
     }
-    const uint64_t nbins = (f->m + (1ull << kSegBits) - 1) >> kSegBits;
-    if (nbins <= kPartMaxBins && n >= (size_t)nbins * 256) return BLOOMHIP_BUILD_PARTITION;
+    // The partition build pays two passes over 12 B/key; below ~64K keys a
+    // direct atomic build is cheaper.
+    if (n >= (1u << 16) && partition_able(f)) return BLOOMHIP_BUILD_PARTITION;
     return BLOOMHIP_BUILD_ATOMIC;
 }
 
@@ -252,8 +258,7 @@ int strategy_supported(const bloomhip_filter *f, int strategy) {
     switch (strategy) {
         case BLOOMHIP_BUILD_ATOMIC: return 1;
         case BLOOMHIP_BUILD_LDS: return f->mp.fast && (f->m + 7) / 8 <= kLdsBitmapBytes;
-        case BLOOMHIP_BUILD_PARTITION:
-            return f->mp.fast && ((f->m + (1ull << kSegBits) - 1) >> kSegBits) <= kPartMaxBins;
+        case BLOOMHIP_BUILD_PARTITION: return partition_able(f);
         default: return 0;
     }
 }
@@ -263,14 +268,8 @@ int strategy_supported(const bloomhip_filter *f, int strategy) {
 int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
                         PartitionWorkspace *out) {
     PartitionWorkspace ws{};
-    ws.nbins = (size_t)((m + (1ull << kSegBits) - 1) >> kSegBits);
+    if (!plan_segments(m, device_cu_count(), &ws)) return BLOOMHIP_ERANGE;
     ws.ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
-    // Pass 2 wants >= ~2 workgroups per CU.  With few segments, each
-    // segment's tiles are split over several workgroups, merged by atomicOr
-    // of their LDS images (cheap next to the positions they read).
-    size_t nsplit = ws.nbins >= 256 ? 1 : (512 + ws.nbins - 1) / ws.nbins;
-    nsplit = std::min(nsplit, ws.ntiles);
-    ws.nsplit = std::max<size_t>(1, nsplit);
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->pos), &w->pos_bytes,
                          ws.ntiles * (size_t)kPartTilePos * 4, s));
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->runs), &w->runs_bytes,
@@ -282,8 +281,7 @@ int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
 }
 
 bool probe_partitioned(const bloomhip_filter *f, int owner_strategy, size_t n) {
-    const bool able = f->mp.fast && ((f->m + (1ull << kSegBits) - 1) >> kSegBits) <= kPartMaxBins;
-    if (!able) return false;
+    if (!partition_able(f)) return false;
     const int st = f->probe_strategy != BLOOMHIP_PROBE_AUTO ? f->probe_strategy : owner_strategy;
     if (st == BLOOMHIP_PROBE_PARTITION) return true;
     if (st == BLOOMHIP_PROBE_GATHER) return false;

@@ -36,14 +36,20 @@ struct ProbeTable {
 // CU on gfx950, one such workgroup per CU.
 constexpr size_t kLdsBitmapBytes = 160 * 1024;
 
-// Partition build geometry: one LDS segment = 2^kSegBits bits.
-constexpr int kSegBits = 19;  // 64 KiB of bitmap per segment workgroup
-constexpr uint32_t kSegMask = (1u << kSegBits) - 1u;
+// Partition build geometry.  Pass 1 counting-sorts positions by sub-segment
+// p >> sub_shift (nsub <= kPartMaxBins sub-segments of 2^sub_shift bits).
+// Pass 2 gives each workgroup g consecutive sub-segments = one segment of
+// S = g << sub_shift bits (S <= kSegMaxBits, so it fits one workgroup's LDS);
+// their runs are adjacent in every sorted tile, so a workgroup still reads one
+// contiguous run per tile.  plan_segments picks (sub_shift, g) so the number
+// of segments is a multiple of the CU count: every CU of pass 2 gets the same
+// share.
+constexpr uint32_t kSegMaxBits = 144u * 1024u * 8u;  // 144 KiB of LDS
 constexpr int kPartBlock = 512;
 constexpr int kPartKPT = 8;  // keys per thread in pass 1
 constexpr size_t kPartTileKeys = (size_t)kPartBlock * kPartKPT;  // 4096
 constexpr int kPartTilePos = (int)kPartTileKeys * 3;
-constexpr size_t kPartMaxBins = 2048;  // m <= 2^30 bits
+constexpr size_t kPartMaxBins = 4096;  // sub-segments sorted by pass 1
 
 // Probe: filters up to this size are gathered directly (they stay resident in
 // every XCD's 4 MiB L2); larger ones use the partitioned probe when the batch
@@ -52,12 +58,21 @@ constexpr size_t kProbeGatherMaxBytes = 2u << 20;
 constexpr size_t kProbePartitionMinKeys = 1u << 18;
 
 struct PartitionWorkspace {
-    uint32_t *pos;         // [ntiles * kPartTilePos] tile-sorted segment offsets
-    uint32_t *run_starts;  // [ntiles * (nbins + 1)]
+    uint32_t *pos;         // [ntiles * kPartTilePos] tile-sorted positions
+    uint32_t *run_starts;  // [ntiles * (nbins + 1)], run starts per pass-2 segment
     size_t ntiles;
-    size_t nbins;
-    size_t nsplit;         // pass-2 workgroups per segment
+    size_t nbins;          // pass-2 segments
+    uint32_t sub_shift;    // pass-1 sub-segment = pos >> sub_shift
+    uint32_t group;        // sub-segments per pass-2 segment
+    uint32_t nsub;         // pass-1 sub-segments
+    uint32_t seg_bits;     // S = group << sub_shift
 };
+
+// CUs of the current device (cached).
+int device_cu_count();
+// Fills the geometry fields of ws for a filter of m bits; false when the
+// partition path does not apply (m >= 2^32).
+bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws);
 
 // Kernels enqueued on `stream`; all return hipSuccess or the launch error.
 hipError_t launch_build_atomic(const KeySpan &keys, const ModParams &mp, uint32_t *words,

@@ -117,11 +117,12 @@ __global__ void __launch_bounds__(kBlock) k_build_lds(KeySpan ks, ModParams mp,
 // ---------------------------------------------------------------------------
 // partition pass 1 (k_part_bin): persistent 512-thread workgroups walk tiles
 // of kPartTileKeys keys.  Each thread hashes kPartKPT keys; the 3 positions
-// are counting-sorted by segment (pos >> kSegBits) in LDS and the sorted tile
-// (segment offsets) is written contiguously to pos_out[tile*kPartTilePos..].
-// Row `tile` of run_starts holds the exclusive prefix of the tile's
-// per-segment counts (nbins + 1 entries), so segment b's run of this tile is
-// [run_starts[tile][b], run_starts[tile][b+1]).  No global atomics.
+// are counting-sorted by sub-segment (pos >> sub_shift) in LDS and the sorted
+// tile (full positions) is written contiguously to pos_out[tile*kPartTilePos..].
+// Row `tile` of run_starts holds, for each pass-2 segment b (= sub-segments
+// [b*group, (b+1)*group)), where its run of this tile starts (nbins + 1
+// entries), so segment b's run is [run_starts[tile][b], run_starts[tile][b+1]).
+// No global atomics.
 //
 // The next tile's keys are loaded while the current tile is sorted, and the
 // workgroup barriers wait only for LDS (lgkmcnt), so the sorted tile's
@@ -156,11 +157,14 @@ __device__ __forceinline__ void load_tile_keys(const KeySpan &ks, size_t tile, i
 
 // ABLATE (timing builds only, tools/ubench): 1 = skip the sorted-tile store,
 // 2 = also skip the LDS scatter, 3 = hash only.  The product launches 0.
-template <int LAYOUT, int ABLATE = 0, bool SLOTS = false>
+// SEG_SORT (timing builds only): sort by pass-2 segment sub / group instead of
+// by sub-segment (same runs, different order inside a run).
+template <int LAYOUT, int ABLATE = 0, bool SLOTS = false, bool SEG_SORT = false>
 __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParams mp,
                                                          uint32_t *__restrict__ pos_out,
                                                          uint32_t *__restrict__ run_starts,
-                                                         int nbins, size_t ntiles,
+                                                         int nbins, int nsub, int sub_shift,
+                                                         int group, size_t ntiles,
                                                          uint16_t *__restrict__ slots) {
     __shared__ __attribute__((aligned(16))) uint32_t s_sorted[kPartTilePos];
     __shared__ uint32_t s_hist[kMaxBins + 1];
@@ -174,13 +178,15 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
     for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t tile0 = tile * kPartTileKeys;
         const int tile_keys = (int)min((size_t)kPartTileKeys, ks.n - tile0);
-        for (int b = tid; b <= nbins; b += kPartBlock) s_hist[b] = 0;
+        for (int b = tid; b <= nsub; b += kPartBlock) s_hist[b] = 0;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
         if (tile + gridDim.x < ntiles) load_tile_keys<LAYOUT>(ks, tile + gridDim.x, tid, knext);
 
-        // 1. positions, and each one's rank inside its segment (LDS atomics).
+        // 1. positions, and each one's rank inside its sub-segment (LDS
+        //    atomics).  br[] keeps (sub-segment << 16) | rank (sub < 4096,
+        //    rank < 12288).
         uint32_t pos[kPartKPT * 3];
-        uint32_t rank[kPartKPT * 3];
+        uint32_t br[kPartKPT * 3];
 #pragma unroll
         for (int j = 0; j < kPartKPT; j++) {
             if (j * kPartBlock + tid < tile_keys) {
@@ -190,8 +196,11 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
                 pos[3 * j + 2] = pos32(raw_hash3(k), mp);
                 if constexpr (ABLATE < 3) {
 #pragma unroll
-                    for (int h = 0; h < 3; h++)
-                        rank[3 * j + h] = atomicAdd(&s_hist[pos[3 * j + h] >> kSegBits], 1u);
+                    for (int h = 0; h < 3; h++) {
+                        uint32_t sub = pos[3 * j + h] >> sub_shift;
+                        if constexpr (SEG_SORT) sub = (sub / (uint32_t)group) * (uint32_t)group;
+                        br[3 * j + h] = (sub << 16) | atomicAdd(&s_hist[sub], 1u);
+                    }
                 }
             }
         }
@@ -206,14 +215,15 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
         }
         lds_barrier();
 
-        // 2. exclusive scan of the nbins+1 counts (the extra slot is 0 and
-        //    receives the tile total).
+        // 2. exclusive scan of the nsub+1 counts (the extra slot is 0 and
+        //    receives the tile total); the run of pass-2 segment b starts at
+        //    sub-segment b*group.
         uint32_t local[kScanPer];
         uint32_t tsum = 0;
 #pragma unroll
         for (int q = 0; q < kScanPer; q++) {
             const int b = tid * kScanPer + q;
-            local[q] = b <= nbins ? s_hist[b] : 0u;
+            local[q] = b <= nsub ? s_hist[b] : 0u;
             tsum += local[q];
         }
         uint32_t incl = tsum;
@@ -226,17 +236,18 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
         lds_barrier();
         uint32_t run = incl - tsum;
         for (int w = 0; w < wave; w++) run += s_wsum[w];
-        uint32_t *row = run_starts + tile * (size_t)(nbins + 1);
 #pragma unroll
         for (int q = 0; q < kScanPer; q++) {
             const int b = tid * kScanPer + q;
-            if (b <= nbins) {
+            if (b <= nsub) {
                 s_hist[b] = run;
-                row[b] = run;
                 run += local[q];
             }
         }
         lds_barrier();
+        uint32_t *row = run_starts + tile * (size_t)(nbins + 1);
+        for (int b = tid; b <= nbins; b += kPartBlock)
+            row[b] = s_hist[b == nbins ? nsub : b * group];
 
         if constexpr (ABLATE < 2) {
             // 3. scatter into the LDS image sorted by segment.
@@ -245,9 +256,9 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
                 if (j * kPartBlock + tid < tile_keys) {
 #pragma unroll
                     for (int h = 0; h < 3; h++) {
-                        const uint32_t p = pos[3 * j + h];
-                        const uint32_t slot = s_hist[p >> kSegBits] + rank[3 * j + h];
-                        s_sorted[slot] = p & kSegMask;
+                        const uint32_t b = br[3 * j + h];
+                        const uint32_t slot = s_hist[b >> 16] + (b & 0xFFFFu);
+                        s_sorted[slot] = pos[3 * j + h];  // full position
                         if constexpr (SLOTS)
                             slots[(tile * 3 + h) * kPartTileKeys + j * kPartBlock + tid] =
                                 (uint16_t)slot;
@@ -274,12 +285,11 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
 }
 
 // ---------------------------------------------------------------------------
-// partition pass 2 (k_part_apply): workgroup (b, split) ORs segment b's runs
-// of tiles [split*tps, (split+1)*tps) into a 64 KiB LDS image, then writes the
-// segment (nsplit == 1: plain 16-B stores, OR-merged with the old bitmap when
-// it may be non-zero; nsplit > 1: atomicOr of the non-zero words).
+// partition pass 2 (k_part_apply): workgroup b ORs segment b's run of every
+// tile into an LDS image of the segment (S bits), then writes the segment
+// out with plain 16-B stores (OR-merged with the old bitmap when that may be
+// non-zero).  Segments never overlap, so no atomics leave the CU.
 // ---------------------------------------------------------------------------
-constexpr int kSegWords = (1 << kSegBits) / 32;  // 16384 u32 = 64 KiB
 
 // Bijective block -> work-unit map that gives each XCD a contiguous range of
 // units (cdna_hip_programming.md §5.5 T1, bijective form for n % 8 != 0).
@@ -295,10 +305,9 @@ constexpr int kApplyBlock = 1024;
 constexpr int kApplyWaves = kApplyBlock / 64;
 constexpr int kApplyChunk = kApplyBlock;  // tiles whose run bounds are staged in LDS at once
 constexpr int kApplyBatch = 16;           // runs per batch; two batches in flight
-// At >= this many segments a tile's runs average <= 48 entries (12288/256).
-constexpr size_t kShortRunBins = 256;
+// At >= this many segments a tile's runs average <= 64 entries (12288/192).
+constexpr size_t kShortRunBins = 192;
 static_assert(kApplyChunk == kApplyWaves * 64, "one 64-tile slice per wave per chunk");
-static_assert(kPartTileKeys <= (1u << (32 - kSegBits)), "probe tags must fit beside the offset");
 
 // PROBE = false: build (OR every entry into the zeroed LDS image, write the
 // segment).  PROBE = true: the LDS image is the filter's segment; each entry's
@@ -308,31 +317,31 @@ static_assert(kPartTileKeys <= (1u << (32 - kSegBits)), "probe tags must fit bes
 // LONG_RUNS: few segments, so runs span several 64-entry steps; the wave
 // walks (batch, offset) steps.  Otherwise runs rarely exceed 64 entries: one
 // step per batch, and the rare longer run finishes in a per-tile tail loop.
-template <bool PROBE, bool LONG_RUNS>
+// ABLATE (timing builds only): 1 = skip the LDS ORs, 2 = skip the position
+// loads (synthetic entries).  The product launches 0.
+template <bool PROBE, bool LONG_RUNS, int BATCH = kApplyBatch, int ABLATE = 0>
 __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
     const uint32_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
-    int nbins, int nsplit, uint32_t *__restrict__ words, uint64_t nw32, int merge_existing,
-    uint8_t *__restrict__ res) {
+    int nbins, uint32_t seg_bits, uint32_t *__restrict__ words, uint64_t nw32,
+    int merge_existing, uint8_t *__restrict__ res) {
+    const uint32_t seg_words = seg_bits / 32;
     extern __shared__ __attribute__((aligned(16))) uint32_t seg[];
     __shared__ uint2 s_run[kApplyChunk];  // (start, end) of this segment's run per tile
     // Neighbouring segments' runs share 128-B lines of every sorted tile, so
     // give consecutive segments to workgroups on one XCD (blocks are dealt
-    // round-robin over the 8 XCDs): block x -> unit (x % 8) * per + x / 8.
-    // A bijection on [0, nunits); placement only affects speed.
-    const unsigned nunits = (unsigned)(nbins * nsplit);
-    const unsigned unit = xcd_remap(blockIdx.x, nunits);
-    const int b = (int)(unit % (unsigned)nbins);
-    const int split = (int)(unit / (unsigned)nbins);
-    const int tps = (ntiles + nsplit - 1) / nsplit;
-    const int t_begin = split * tps;
-    const int t_end = min(ntiles, t_begin + tps);
+    // round-robin over the 8 XCDs): a bijection on [0, nbins); placement only
+    // affects speed.
+    const int b = (int)xcd_remap(blockIdx.x, (unsigned)nbins);
+    const int t_begin = 0;
+    const int t_end = ntiles;
+    const uint64_t w0 = (uint64_t)b * seg_words;
+    const int nseg = (int)(min(nw32, w0 + seg_words) - w0);  // last segment may be short
+    const uint32_t base = (uint32_t)b * seg_bits;             // entries are full positions
     if constexpr (PROBE) {
-        const uint64_t w0 = (uint64_t)b * kSegWords;
-        const int nseg = (int)(min(nw32, w0 + kSegWords) - w0);
-        for (int i = threadIdx.x; i < kSegWords; i += kApplyBlock)
+        for (int i = threadIdx.x; i < (int)seg_words; i += kApplyBlock)
             seg[i] = i < nseg ? words[w0 + i] : 0u;
     } else {
-        for (int i = threadIdx.x; i < kSegWords / 4; i += kApplyBlock)
+        for (int i = threadIdx.x; i < (int)seg_words / 4; i += kApplyBlock)
             reinterpret_cast<uint4 *>(seg)[i] = make_uint4(0, 0, 0, 0);
     }
 
@@ -352,20 +361,20 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
         __syncthreads();
         r_next = fetch_run(c0 + kApplyChunk + (int)threadIdx.x);
         // wave w owns tiles c0 + 64w .. c0 + 64w + 63 of this chunk; its runs
-        // are read kApplyBatch at a time, the next batch's loads issued before
+        // are read BATCH at a time, the next batch's loads issued before
         // the current batch's LDS ORs.
         const int wt0 = wave * 64;
         const int wtn = max(0, min(64, t_end - (c0 + wt0)));
         const uint32_t *wbase = pos + (size_t)(c0 + wt0) * kPartTilePos;
         // The wave's work is a sequence of steps (k0, off): entries
-        // [off, off + 64) of the runs of tiles k0 .. k0 + kApplyBatch - 1.
+        // [off, off + 64) of the runs of tiles k0 .. k0 + BATCH - 1.
         // Loads of the next step are issued before the current step's LDS
-        // work, so two steps (2 * kApplyBatch loads per lane) are in flight.
-        uint32_t cur[kApplyBatch], nxt[kApplyBatch];
+        // work, so two steps (2 * BATCH loads per lane) are in flight.
+        uint32_t cur[BATCH], nxt[BATCH];
         auto batch_maxlen = [&](int k0) -> uint32_t {
             uint32_t ml = 0;
 #pragma unroll
-            for (int k = 0; k < kApplyBatch; k++) {
+            for (int k = 0; k < BATCH; k++) {
                 if (k0 + k < wtn) {
                     const uint2 r = s_run[wt0 + k0 + k];
                     ml = max(ml, r.y - r.x);
@@ -373,25 +382,34 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
             }
             return __builtin_amdgcn_readfirstlane(ml);
         };
-        auto load_step = [&](int k0, uint32_t off, uint32_t (&v)[kApplyBatch]) {
+        auto load_step = [&](int k0, uint32_t off, uint32_t (&v)[BATCH]) {
 #pragma unroll
-            for (int k = 0; k < kApplyBatch; k++) {
+            for (int k = 0; k < BATCH; k++) {
                 const uint2 r = k0 + k < wtn ? s_run[wt0 + k0 + k] : make_uint2(0, 0);
                 const uint32_t e = r.x + off + lane;
-                v[k] = e < r.y ? wbase[(size_t)(k0 + k) * kPartTilePos + e] : 0xFFFFFFFFu;
+                if constexpr (ABLATE == 2)
+                    v[k] = e < r.y ? ((e * 2654435761u) >> 13) % 524288u : 0xFFFFFFFFu;
+                else
+                    // raw position; `base` is subtracted where it is consumed,
+                    // so the load stays in flight until apply_step
+                    v[k] = e < r.y ? wbase[(size_t)(k0 + k) * kPartTilePos + e] : 0xFFFFFFFFu;
             }
         };
-        auto apply_step = [&](int k0, uint32_t off, const uint32_t (&v)[kApplyBatch]) {
+        auto apply_step = [&](int k0, uint32_t off, const uint32_t (&v)[BATCH]) {
 #pragma unroll
-            for (int k = 0; k < kApplyBatch; k++) {
+            for (int k = 0; k < BATCH; k++) {
                 if (v[k] == 0xFFFFFFFFu) continue;
+                const uint32_t o = v[k] - (ABLATE == 2 ? 0u : base);
                 if constexpr (PROBE) {
                     const uint32_t e = s_run[wt0 + k0 + k].x + off + lane;
                     res[(size_t)(c0 + wt0 + k0 + k) * kPartTilePos + e] =
-                        (seg[v[k] >> 5] >> (v[k] & 31)) & 1u;
+                        (seg[o >> 5] >> (o & 31)) & 1u;
+                } else if constexpr (ABLATE == 1) {
+                    (void)off;
+                    asm volatile("" ::"v"(o));
                 } else {
                     (void)off;
-                    atomicOr(&seg[v[k] >> 5], 1u << (v[k] & 31));
+                    atomicOr(&seg[o >> 5], 1u << (o & 31));
                 }
             }
         };
@@ -404,7 +422,7 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
                 int nk0 = k0;
                 uint32_t noff = off + 64, nml = ml;
                 if (noff >= ml) {
-                    nk0 = k0 + kApplyBatch;
+                    nk0 = k0 + BATCH;
                     noff = 0;
                     nml = nk0 < wtn ? batch_maxlen(nk0) : 0;
                 }
@@ -413,23 +431,23 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
                 apply_step(k0, off, cur);
                 if (!more) break;
 #pragma unroll
-                for (int k = 0; k < kApplyBatch; k++) cur[k] = nxt[k];
+                for (int k = 0; k < BATCH; k++) cur[k] = nxt[k];
                 k0 = nk0;
                 off = noff;
                 ml = nml;
             }
         } else {
             load_step(0, 0, cur);
-            for (int k0 = 0; k0 < wtn; k0 += kApplyBatch) {
-                if (k0 + kApplyBatch < wtn) load_step(k0 + kApplyBatch, 0, nxt);
+            for (int k0 = 0; k0 < wtn; k0 += BATCH) {
+                if (k0 + BATCH < wtn) load_step(k0 + BATCH, 0, nxt);
                 apply_step(k0, 0, cur);
 #pragma unroll
-                for (int k = 0; k < kApplyBatch; k++) cur[k] = nxt[k];
+                for (int k = 0; k < BATCH; k++) cur[k] = nxt[k];
             }
             for (int k = 0; k < wtn; k++) {  // entries past the first 64 of a run
                 const uint2 r = s_run[wt0 + k];
                 for (uint32_t e = r.x + 64 + lane; e < r.y; e += 64) {
-                    const uint32_t v = wbase[(size_t)k * kPartTilePos + e];
+                    const uint32_t v = wbase[(size_t)k * kPartTilePos + e] - base;
                     if constexpr (PROBE) {
                         res[(size_t)(c0 + wt0 + k) * kPartTilePos + e] =
                             (seg[v >> 5] >> (v & 31)) & 1u;
@@ -443,19 +461,11 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
     if constexpr (PROBE) return;
     __syncthreads();
 
-    const uint64_t w0 = (uint64_t)b * kSegWords;
-    const uint64_t wend = min(nw32, w0 + kSegWords);
-    const int nseg = (int)(wend - w0);
     uint32_t *dst = words + w0;
-    if (nsplit > 1) {
-        for (int i = threadIdx.x; i < nseg; i += kApplyBlock) {
-            const uint32_t w = seg[i];
-            if (w) __hip_atomic_fetch_or(dst + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else if (nseg == kSegWords) {
+    if (nseg == (int)seg_words) {  // seg_words % 4 == 0 and w0 is 16-B aligned
         uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
         const uint4 *seg4 = reinterpret_cast<const uint4 *>(seg);
-        for (int q = threadIdx.x; q < kSegWords / 4; q += kApplyBlock) {
+        for (int q = threadIdx.x; q < (int)seg_words / 4; q += kApplyBlock) {
             uint4 v = seg4[q];
             if (merge_existing) {
                 const uint4 o = dst4[q];
@@ -555,20 +565,9 @@ __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     }
 }
 
-// Persistent pass-1 grid: two 57-KiB-LDS workgroups per CU.
+// Persistent pass-1 grid: two 64-KiB-LDS workgroups per CU.
 inline unsigned part_bin_grid(size_t ntiles) {
-    static int cus[64] = {0};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64) dev = 0;
-    if (cus[dev] == 0) {
-        int c = 0;
-        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            c <= 0)
-            c = 256;
-        cus[dev] = c;
-    }
-    const size_t g = (size_t)cus[dev] * 2;
+    const size_t g = (size_t)device_cu_count() * 2;
     return (unsigned)(ntiles < g ? ntiles : g);
 }
 
@@ -628,16 +627,74 @@ hipError_t launch_build_lds(const KeySpan &ks, const ModParams &mp, uint32_t *wo
     return hipGetLastError();
 }
 
+int device_cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (cus[dev] == 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            c <= 0)
+            c = 256;
+        cus[dev] = c;
+    }
+    return cus[dev];
+}
+
+bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
+    if (m == 0 || m > 0xFFFFFFFFull || ncu <= 0) return false;
+    // Pass-2 segments: a multiple W of the CU count, each fitting in LDS.
+    const uint64_t per_round = (uint64_t)ncu * kSegMaxBits;
+    const uint64_t W = ((m + per_round - 1) / per_round) * (uint64_t)ncu;
+    // Sub-segments: the smallest power of two 2^s with at most kPartMaxBins
+    // of them, then g = ceil(nsub / W) per segment, while g << s fits LDS.
+    uint32_t s = 5;  // >= one 32-bit word
+    while ((((m - 1) >> s) + 1) > kPartMaxBins) s++;
+    uint64_t nsub = ((m - 1) >> s) + 1;
+    uint64_t g = (nsub + W - 1) / W;
+    while (g > 1 && (g << s) > kSegMaxBits) g--;
+    if ((g << s) > kSegMaxBits) return false;
+    // 128-B aligned segments for the 16-B segment stores.
+    while (((g << s) % 1024) != 0) g++;
+    if ((g << s) > kSegMaxBits) return false;
+    ws->sub_shift = s;
+    ws->group = (uint32_t)g;
+    ws->nsub = (uint32_t)nsub;
+    ws->seg_bits = (uint32_t)(g << s);
+    ws->nbins = (size_t)((nsub + g - 1) / g);
+    return true;
+}
+
 hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                            hipStream_t stream) {
     if (ks.n == 0) return hipSuccess;
     const unsigned grid = part_bin_grid(ws.ntiles);
     if (ks.layout == KEYS_PACKED)
         k_part_bin<KEYS_PACKED><<<grid, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, ws.ntiles, nullptr);
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, (int)ws.nsub, (int)ws.sub_shift,
+            (int)ws.group, ws.ntiles, nullptr);
     else
         k_part_bin<KEYS_STRIDED><<<grid, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, ws.ntiles, nullptr);
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, (int)ws.nsub, (int)ws.sub_shift,
+            (int)ws.group, ws.ntiles, nullptr);
+    return hipGetLastError();
+}
+
+// Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
+// must be opted into per kernel).
+template <bool PROBE, bool LONG_RUNS>
+hipError_t launch_apply(const PartitionWorkspace &ws, uint32_t *words, uint64_t nw32, int merge,
+                        uint8_t *res, hipStream_t stream) {
+    static const bool attr_set = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<PROBE, LONG_RUNS>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(kSegMaxBits / 8));
+        return true;
+    }();
+    (void)attr_set;
+    k_part_apply<PROBE, LONG_RUNS><<<(unsigned)ws.nbins, kApplyBlock, ws.seg_bits / 8, stream>>>(
+        ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, words, nw32, merge, res);
     return hipGetLastError();
 }
 
@@ -645,16 +702,9 @@ hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const Partiti
                              int merge_existing, hipStream_t stream) {
     if (ws.ntiles == 0) return hipSuccess;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
-    const unsigned grid = (unsigned)(ws.nbins * ws.nsplit);
     if (ws.nbins >= kShortRunBins)
-        k_part_apply<false, false><<<grid, kApplyBlock, kSegWords * 4, stream>>>(
-            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit, words, nw32,
-            merge_existing, nullptr);
-    else
-        k_part_apply<false, true><<<grid, kApplyBlock, kSegWords * 4, stream>>>(
-            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit, words, nw32,
-            merge_existing, nullptr);
-    return hipGetLastError();
+        return launch_apply<false, false>(ws, words, nw32, merge_existing, nullptr, stream);
+    return launch_apply<false, true>(ws, words, nw32, merge_existing, nullptr, stream);
 }
 
 hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, const uint32_t *words,
@@ -664,23 +714,18 @@ hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, cons
     const unsigned g1 = part_bin_grid(ws.ntiles);
     if (ks.layout == KEYS_PACKED)
         k_part_bin<KEYS_PACKED, 0, true><<<g1, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, ws.ntiles, slots);
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, (int)ws.nsub, (int)ws.sub_shift,
+            (int)ws.group, ws.ntiles, slots);
     else
         k_part_bin<KEYS_STRIDED, 0, true><<<g1, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, ws.ntiles, slots);
+            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, (int)ws.nsub, (int)ws.sub_shift,
+            (int)ws.group, ws.ntiles, slots);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
-    const unsigned g2 = (unsigned)(ws.nbins * ws.nsplit);
-    if (ws.nbins >= kShortRunBins)
-        k_part_apply<true, false><<<g2, kApplyBlock, kSegWords * 4, stream>>>(
-            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit,
-            const_cast<uint32_t *>(words), nw32, 0, res);
-    else
-        k_part_apply<true, true><<<g2, kApplyBlock, kSegWords * 4, stream>>>(
-            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, (int)ws.nsplit,
-            const_cast<uint32_t *>(words), nw32, 0, res);
-    e = hipGetLastError();
+    uint32_t *w = const_cast<uint32_t *>(words);  // read-only in PROBE mode
+    e = ws.nbins >= kShortRunBins ? launch_apply<true, false>(ws, w, nw32, 0, res, stream)
+                                  : launch_apply<true, true>(ws, w, nw32, 0, res, stream);
     if (e != hipSuccess) return e;
     k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out);
     return hipGetLastError();

@@ -104,6 +104,32 @@ BH_HD uint64_t mod_any(uint64_t x, const ModParams &p) {
     return p.fast ? (uint64_t)mod_fast(x, p) : x % p.m;
 }
 
+// ---- exact q = x / S for 32-bit x, runtime S >= 2 (Granlund–Montgomery,
+// "Division by invariant integers using multiplication", PLDI 1994, Fig 4.1):
+// l = ceil(log2 S), M = floor(2^32 (2^l - S) / S) + 1,
+// q = (t + ((x - t) >> 1)) >> (l - 1) with t = mulhi(M, x).
+struct DivParams {
+    uint32_t S;
+    uint32_t M;
+    uint32_t sh;  // l - 1
+    uint32_t pad;
+};
+
+inline DivParams make_div_params(uint32_t S) {
+    DivParams d{};
+    d.S = S;
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < S) l++;
+    d.M = (uint32_t)(((1ull << 32) * ((1ull << l) - S)) / S + 1);
+    d.sh = l - 1;
+    return d;
+}
+
+BH_HD uint32_t div_fast(uint32_t x, const DivParams &d) {
+    const uint32_t t = (uint32_t)(((uint64_t)d.M * x) >> 32);
+    return (t + ((x - t) >> 1)) >> d.sh;
+}
+
 BH_HD void positions3(int32_t k, const ModParams &p, uint64_t out[3]) {
     out[0] = mod_any(raw_hash1(k), p);
     out[1] = mod_any(raw_hash2(k), p);

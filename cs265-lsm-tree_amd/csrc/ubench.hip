@@ -110,15 +110,49 @@ extern "C" int ubench_part_bin(int ablate, const void *keys, size_t n, uint64_t 
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
     const ModParams mp = make_mod_params(m);
-    const int nbins = (int)((m + (1ull << kSegBits) - 1) >> kSegBits);
+    PartitionWorkspace ws{};
+    if (!plan_segments(m, device_cu_count(), &ws)) return -34;
+    const int nbins = (int)ws.nbins;
     const size_t ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
     const unsigned grid = part_bin_grid(ntiles);
+    const int nsub = (int)ws.nsub, ssh = (int)ws.sub_shift, grp = (int)ws.group;
     switch (ablate) {
-        case 0: k_part_bin<KEYS_PACKED, 0><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, ntiles, nullptr); break;
-        case 1: k_part_bin<KEYS_PACKED, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, ntiles, nullptr); break;
-        case 2: k_part_bin<KEYS_PACKED, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, ntiles, nullptr); break;
-        case 3: k_part_bin<KEYS_PACKED, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, ntiles, nullptr); break;
+        case 0: k_part_bin<KEYS_PACKED, 0><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 1: k_part_bin<KEYS_PACKED, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 2: k_part_bin<KEYS_PACKED, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 3: k_part_bin<KEYS_PACKED, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 10: k_part_bin<KEYS_PACKED, 0, false, true><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
         default: return -22;
     }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Pass 2 of the partition build (variants: 16 = product, 101 = loads only,
+// 102 = LDS only), on the positions of ubench_part_bin ablate 0.
+extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_t *run_starts,
+                                 size_t n, uint64_t m, uint32_t *words, void *stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    PartitionWorkspace ws{};
+    if (!plan_segments(m, device_cu_count(), &ws)) return -34;
+    const int nbins = (int)ws.nbins;
+    const int ntiles = (int)((n + kPartTileKeys - 1) / kPartTileKeys);
+    const uint64_t nw32 = ((m + 63) / 64) * 2;
+    const uint32_t sb = ws.seg_bits;
+#define UB_APPLY(B, A)                                                                        \
+    do {                                                                                      \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<false, false, B, A>), \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,                 \
+                                  (int)(kSegMaxBits / 8));                                    \
+        k_part_apply<false, false, B, A><<<nbins, kApplyBlock, sb / 8, s>>>(                  \
+            pos, run_starts, ntiles, nbins, sb, words, nw32, 0, nullptr);                     \
+    } while (0)
+    switch (variant) {
+        case 8: UB_APPLY(8, 0); break;
+        case 16: UB_APPLY(16, 0); break;
+        case 101: UB_APPLY(16, 1); break;
+        case 102: UB_APPLY(16, 2); break;
+        default: return -22;
+    }
+#undef UB_APPLY
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -18,6 +18,9 @@ LIB.ubench_run.restype = ctypes.c_int
 LIB.ubench_part_bin.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 LIB.ubench_part_bin.restype = ctypes.c_int
+LIB.ubench_part_apply.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+LIB.ubench_part_apply.restype = ctypes.c_int
 
 
 def timeit(which, buf, nbytes, m, grid, block, iters, reps=5):
@@ -41,7 +44,7 @@ def part_ablation():
     keys = torch.from_numpy(bh.gen_puts(13141, 16_777_216)).cuda()
     m = 167_772_160
     ntiles = (keys.numel() + 4095) // 4096
-    nbins = (m + (1 << 19) - 1) >> 19
+    nbins = 4096  # upper bound for the run-start table
     pos = torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda")
     rs = torch.empty(ntiles * (nbins + 1), dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
@@ -60,10 +63,33 @@ def part_ablation():
         torch.cuda.synchronize()
         print(json.dumps({"op": "k_part_bin", "ablate": names[ab],
                           "us": round(a.elapsed_time(b) / 10 * 1e3, 2)}), flush=True)
+    # pass 2 variants on the positions of a full pass 1 (sub-segment order,
+    # then segment order)
+    words = torch.zeros((m + 63) // 64 * 2, dtype=torch.int32, device="cuda")
+    for layout, ab in (("sub-sorted", 0), ("seg-sorted", 10)):
+        LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(), rs.data_ptr(),
+                            s.cuda_stream)
+        torch.cuda.synchronize()
+        for batch in (16, 101, 102):
+            for _ in range(2):
+                LIB.ubench_part_apply(batch, pos.data_ptr(), rs.data_ptr(), keys.numel(), m,
+                                      words.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            for _ in range(10):
+                LIB.ubench_part_apply(batch, pos.data_ptr(), rs.data_ptr(), keys.numel(), m,
+                                      words.data_ptr(), s.cuda_stream)
+            b.record(s)
+            torch.cuda.synchronize()
+            print(json.dumps({"op": "k_part_apply", "layout": layout, "variant": batch,
+                              "us": round(a.elapsed_time(b) / 10 * 1e3, 2)}), flush=True)
 
 
 def main():
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "isa":
+        return isa_rates()
     if len(sys.argv) > 1 and sys.argv[1] == "part":
         return part_ablation()
     grid, block = 2048, 256
