@@ -90,7 +90,8 @@ struct bloomhip_filter {
     ModParams mp{};
     int strategy = BLOOMHIP_BUILD_AUTO;
     int probe_strategy = BLOOMHIP_PROBE_AUTO;
-    bool known_zero = true;  // host-side knowledge that every bit is 0
+    bool known_zero = true;      // host-side knowledge that every bit is 0
+    bool pending_clear = false;  // cleared, but the memset is not issued yet
 
     std::mutex mu;  // guards staging, workspace and profiling state
     void *d_stage = nullptr;
@@ -291,6 +292,16 @@ bool probe_partitioned(const bloomhip_filter *f, int owner_strategy, size_t n) {
     return (f->m + 7) / 8 > kProbeGatherMaxBytes && n >= kProbePartitionMinKeys;
 }
 
+// Issues a clear() that was deferred (see bloomhip_clear) on stream s.
+int materialize_clear(bloomhip_filter *f, hipStream_t s) {
+    if (!f->pending_clear) return BLOOMHIP_OK;
+    hipError_t e = timed(f, SLOT_CLEAR, s,
+                         [&] { return hipMemsetAsync(f->d_words, 0, f->nwords64 * 8, s); });
+    if (e != hipSuccess) return fail_hip(e, "hipMemsetAsync(bitmap)");
+    f->pending_clear = false;
+    return BLOOMHIP_OK;
+}
+
 int run_partition(bloomhip_filter *f, const KeySpan &ks, hipStream_t s) {
     Workspace *w = workspace_for(f->device, s);
     std::lock_guard<std::mutex> lk(w->mu);
@@ -423,6 +434,15 @@ int bloomhip_device(const bloomhip_filter *f, int *device_out) {
 int bloomhip_device_words(const bloomhip_filter *f, void **dptr_out) {
     g_last_error.clear();
     if (!f || !dptr_out) return BLOOMHIP_EINVAL;
+    {
+        // A deferred clear is issued on the default stream before the raw
+        // pointer is handed out.
+        bloomhip_filter *fm = const_cast<bloomhip_filter *>(f);
+        DeviceGuard g(f->device);
+        std::lock_guard<std::mutex> lk(fm->mu);
+        int rc = materialize_clear(fm, nullptr);
+        if (rc) return rc;
+    }
     *dptr_out = f->d_words;
     return BLOOMHIP_OK;
 }
@@ -437,12 +457,12 @@ int bloomhip_stream(const bloomhip_filter *f, void **stream_out) {
 int bloomhip_clear(bloomhip_filter *f, void *stream) {
     g_last_error.clear();
     if (!f) return BLOOMHIP_EINVAL;
-    DeviceGuard g(f->device);
     std::lock_guard<std::mutex> lk(f->mu);
-    hipStream_t s = pick_stream(f, stream);
-    hipError_t e = timed(f, SLOT_CLEAR, s,
-                         [&] { return hipMemsetAsync(f->d_words, 0, f->nwords64 * 8, s); });
-    if (e != hipSuccess) return fail_hip(e, "hipMemsetAsync(bitmap)");
+    (void)stream;
+    // Deferred: a partition build overwrites every segment, so a clear that
+    // is followed by one needs no memset.  Anything else that touches the
+    // bitmap first issues the memset on its own stream (materialize_clear).
+    f->pending_clear = true;
     f->known_zero = true;
     return BLOOMHIP_OK;
 }
@@ -459,6 +479,12 @@ int bloomhip_set_batch(bloomhip_filter *f, const void *keys, size_t n, size_t st
     if (rc) return rc;
     const int strategy = resolve_strategy(f, n);
     if (!strategy_supported(f, strategy)) return BLOOMHIP_EINVAL;
+    if (strategy == BLOOMHIP_BUILD_PARTITION && f->pending_clear) {
+        f->pending_clear = false;  // pass 2 writes every word with merge = 0
+    } else {
+        rc = materialize_clear(f, s);
+        if (rc) return rc;
+    }
     hipError_t e = hipSuccess;
     switch (strategy) {
         case BLOOMHIP_BUILD_LDS:
@@ -494,6 +520,16 @@ int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const voi
     KeySpan ks{};
     int rc = device_keys(f0, keys, n, stride_bytes, keys_on_device, s, &ks);
     if (rc) return rc;
+    for (int j = 0; j < nf; j++) {
+        bloomhip_filter *fj = const_cast<bloomhip_filter *>(filters[j]);
+        if (fj != f0) {
+            std::lock_guard<std::mutex> lj(fj->mu);
+            rc = materialize_clear(fj, s);
+        } else {
+            rc = materialize_clear(fj, s);
+        }
+        if (rc) return rc;
+    }
     const size_t nw = (n + 63) / 64;
     const size_t out_bytes = (size_t)nf * nw * 8;
     uint64_t *dout = out_packed;
@@ -571,6 +607,12 @@ int bloomhip_download(const bloomhip_filter *f, uint64_t *words, size_t nwords, 
     if (!f || !words || nwords != f->nwords64) return BLOOMHIP_EINVAL;
     DeviceGuard g(f->device);
     hipStream_t s = pick_stream(f, stream);
+    {
+        bloomhip_filter *fm = const_cast<bloomhip_filter *>(f);
+        std::lock_guard<std::mutex> lk(fm->mu);
+        int rc = materialize_clear(fm, s);
+        if (rc) return rc;
+    }
     HIP_TRY(hipMemcpyAsync(words, f->d_words, nwords * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return BLOOMHIP_OK;
@@ -586,6 +628,7 @@ int bloomhip_upload(bloomhip_filter *f, const uint64_t *words, size_t nwords, vo
     hipStream_t s = pick_stream(f, stream);
     HIP_TRY(hipMemcpyAsync(f->d_words, words, nwords * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));
+    f->pending_clear = false;
     f->known_zero = false;
     return BLOOMHIP_OK;
 }

@@ -305,8 +305,12 @@ constexpr int kApplyBlock = 1024;
 constexpr int kApplyWaves = kApplyBlock / 64;
 constexpr int kApplyChunk = kApplyBlock;  // tiles whose run bounds are staged in LDS at once
 constexpr int kApplyBatch = 16;           // runs per batch; two batches in flight
-// At >= this many segments a tile's runs average <= 64 entries (12288/192).
+// At >= this many segments a tile's runs average <= 64 entries (12288/192);
+// at >= kFlatRunBins they average <= 24 and are walked flattened.
 constexpr size_t kShortRunBins = 192;
+constexpr size_t kFlatRunBins = 512;
+constexpr int kFlatDepth = 16;  // 64-entry loads a wave has in flight
+constexpr int kRunsShort = 0, kRunsLong = 1, kRunsFlat = 2;
 static_assert(kApplyChunk == kApplyWaves * 64, "one 64-tile slice per wave per chunk");
 
 // PROBE = false: build (OR every entry into the zeroed LDS image, write the
@@ -314,12 +318,18 @@ static_assert(kApplyChunk == kApplyWaves * 64, "one 64-tile slice per wave per c
 // bit is written as one result byte at the entry's own index in the sorted
 // tile (res[tile*kPartTilePos + index]), so the result stores follow the runs
 // and coalesce like the loads.
-// LONG_RUNS: few segments, so runs span several 64-entry steps; the wave
-// walks (batch, offset) steps.  Otherwise runs rarely exceed 64 entries: one
-// step per batch, and the rare longer run finishes in a per-tile tail loop.
+// RUNS selects how a wave walks its tiles' runs:
+//   kRunsShort: runs rarely exceed 64 entries: one load per run, BATCH runs
+//               per step, the rare longer run finishes in a per-tile tail.
+//   kRunsLong:  few segments, runs span several 64-entry steps; the wave
+//               walks (batch, offset) steps.
+//   kRunsFlat:  many segments, runs much shorter than 64 entries: the wave
+//               concatenates its 64 tiles' runs and walks them 64 entries per
+//               load, each lane finding its tile by binary search over the
+//               run prefix sums held one per lane (ds_bpermute).
 // ABLATE (timing builds only): 1 = skip the LDS ORs, 2 = skip the position
 // loads (synthetic entries).  The product launches 0.
-template <bool PROBE, bool LONG_RUNS, int BATCH = kApplyBatch, int ABLATE = 0>
+template <bool PROBE, int RUNS, int BATCH = kApplyBatch, int ABLATE = 0>
 __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
     const uint32_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, uint32_t seg_bits, uint32_t *__restrict__ words, uint64_t nw32,
@@ -414,7 +424,49 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
             }
         };
         if (wtn <= 0) continue;
-        if constexpr (LONG_RUNS) {
+        if constexpr (RUNS == kRunsFlat) {
+            // lane t: tile t's run length L, its exclusive prefix P and the
+            // offset O mapping a concatenated index e to wbase[e + O].
+            uint32_t L = 0, O = 0;
+            if (lane < wtn) {
+                const uint2 r = s_run[wt0 + lane];
+                L = r.y - r.x;
+                O = (uint32_t)lane * kPartTilePos + r.x;
+            }
+            uint32_t incl = L;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += t;
+            }
+            const uint32_t P = incl - L;
+            O -= P;
+            const uint32_t T = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
+            for (uint32_t s0 = 0; s0 < T; s0 += 64 * kFlatDepth) {
+                uint32_t v[kFlatDepth], idx[kFlatDepth];
+#pragma unroll
+                for (int d = 0; d < kFlatDepth; d++) {
+                    const uint32_t e = s0 + (uint32_t)d * 64 + lane;
+                    int lo = 0;  // largest tile with P <= e (P is non-decreasing)
+#pragma unroll
+                    for (int st = 32; st >= 1; st >>= 1) {
+                        const uint32_t pc = __shfl(P, lo + st, 64);
+                        if (pc <= e) lo += st;
+                    }
+                    idx[d] = e + __shfl(O, lo, 64);
+                    v[d] = e < T ? wbase[idx[d]] : 0xFFFFFFFFu;
+                }
+#pragma unroll
+                for (int d = 0; d < kFlatDepth; d++) {
+                    if (v[d] == 0xFFFFFFFFu) continue;
+                    const uint32_t o = v[d] - base;
+                    if constexpr (PROBE)
+                        res[(size_t)(c0 + wt0) * kPartTilePos + idx[d]] = (seg[o >> 5] >> (o & 31)) & 1u;
+                    else
+                        atomicOr(&seg[o >> 5], 1u << (o & 31));
+                }
+            }
+        } else if constexpr (RUNS == kRunsLong) {
             int k0 = 0;
             uint32_t off = 0, ml = batch_maxlen(0);
             load_step(k0, off, cur);
@@ -683,17 +735,17 @@ hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const Partiti
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
-template <bool PROBE, bool LONG_RUNS>
+template <bool PROBE, int RUNS>
 hipError_t launch_apply(const PartitionWorkspace &ws, uint32_t *words, uint64_t nw32, int merge,
                         uint8_t *res, hipStream_t stream) {
     static const bool attr_set = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<PROBE, LONG_RUNS>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<PROBE, RUNS>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kSegMaxBits / 8));
         return true;
     }();
     (void)attr_set;
-    k_part_apply<PROBE, LONG_RUNS><<<(unsigned)ws.nbins, kApplyBlock, ws.seg_bits / 8, stream>>>(
+    k_part_apply<PROBE, RUNS><<<(unsigned)ws.nbins, kApplyBlock, ws.seg_bits / 8, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, words, nw32, merge, res);
     return hipGetLastError();
 }
@@ -702,9 +754,11 @@ hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const Partiti
                              int merge_existing, hipStream_t stream) {
     if (ws.ntiles == 0) return hipSuccess;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
+    if (ws.nbins >= kFlatRunBins)
+        return launch_apply<false, kRunsFlat>(ws, words, nw32, merge_existing, nullptr, stream);
     if (ws.nbins >= kShortRunBins)
-        return launch_apply<false, false>(ws, words, nw32, merge_existing, nullptr, stream);
-    return launch_apply<false, true>(ws, words, nw32, merge_existing, nullptr, stream);
+        return launch_apply<false, kRunsShort>(ws, words, nw32, merge_existing, nullptr, stream);
+    return launch_apply<false, kRunsLong>(ws, words, nw32, merge_existing, nullptr, stream);
 }
 
 hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, const uint32_t *words,
@@ -724,8 +778,9 @@ hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, cons
     if (e != hipSuccess) return e;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
     uint32_t *w = const_cast<uint32_t *>(words);  // read-only in PROBE mode
-    e = ws.nbins >= kShortRunBins ? launch_apply<true, false>(ws, w, nw32, 0, res, stream)
-                                  : launch_apply<true, true>(ws, w, nw32, 0, res, stream);
+    e = ws.nbins >= kFlatRunBins    ? launch_apply<true, kRunsFlat>(ws, w, nw32, 0, res, stream)
+        : ws.nbins >= kShortRunBins ? launch_apply<true, kRunsShort>(ws, w, nw32, 0, res, stream)
+                                    : launch_apply<true, kRunsLong>(ws, w, nw32, 0, res, stream);
     if (e != hipSuccess) return e;
     k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out);
     return hipGetLastError();

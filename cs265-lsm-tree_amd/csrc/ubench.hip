@@ -140,15 +140,24 @@ extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_
     const uint32_t sb = ws.seg_bits;
 #define UB_APPLY(B, A)                                                                        \
     do {                                                                                      \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<false, false, B, A>), \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<false, kRunsShort, B, A>), \
                                   hipFuncAttributeMaxDynamicSharedMemorySize,                 \
                                   (int)(kSegMaxBits / 8));                                    \
-        k_part_apply<false, false, B, A><<<nbins, kApplyBlock, sb / 8, s>>>(                  \
+        k_part_apply<false, kRunsShort, B, A><<<nbins, kApplyBlock, sb / 8, s>>>(                  \
             pos, run_starts, ntiles, nbins, sb, words, nw32, 0, nullptr);                     \
     } while (0)
     switch (variant) {
         case 8: UB_APPLY(8, 0); break;
         case 16: UB_APPLY(16, 0); break;
+        case 24: UB_APPLY(24, 0); break;
+        case 32: UB_APPLY(32, 0); break;
+        case 48: UB_APPLY(48, 0); break;
+        case 200:  // flattened walk
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<false, kRunsFlat>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kSegMaxBits / 8));
+            k_part_apply<false, kRunsFlat><<<nbins, kApplyBlock, sb / 8, s>>>(
+                pos, run_starts, ntiles, nbins, sb, words, nw32, 0, nullptr);
+            break;
         case 101: UB_APPLY(16, 1); break;
         case 102: UB_APPLY(16, 2); break;
         default: return -22;

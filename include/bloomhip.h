@@ -88,13 +88,16 @@ int bloomhip_size(const bloomhip_filter *f, uint64_t *m_out);
 int bloomhip_nwords(const bloomhip_filter *f, uint64_t *nwords_out);
 int bloomhip_device(const bloomhip_filter *f, int *device_out);
 /* Device address of the bitmap (ceil(m/64) uint64 blocks), for zero-copy
- * interop.  Valid until bloomhip_destroy. */
+ * interop.  Valid until bloomhip_destroy.  A deferred clear is issued on the
+ * default stream first. */
 int bloomhip_device_words(const bloomhip_filter *f, void **dptr_out);
 /* A non-blocking stream owned by the handle, for callers that want the
  * filter's work off the default stream (pass it as `stream`). */
 int bloomhip_stream(const bloomhip_filter *f, void **stream_out);
 
-/* Reset every bit to 0. */
+/* Reset every bit to 0.  The memset is deferred: a following partition
+ * build overwrites every word anyway, and any other use of the bitmap issues
+ * it first on that use's stream. */
 int bloomhip_clear(bloomhip_filter *f, void *stream);
 
 /* BloomFilter::set for keys[0..n): src/bloom_filter.cpp:49-53, as called per

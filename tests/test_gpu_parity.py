@@ -48,7 +48,8 @@ def torch_cuda():
 
 # ---------------------------------------------------------------- build ----
 @pytest.mark.parametrize("m", [1, 2, 31, 32, 33, 64, 65, 256, 1000, 65_537, 512_000, 524_288,
-                               1_000_003, 4_194_304, 10_485_761, 167_772_160])
+                               1_000_003, 4_194_304, 10_485_761, 167_772_160, 671_088_640,
+                               2**32 - 1])
 @pytest.mark.parametrize("strategy", STRATEGIES, ids=["atomic", "lds", "partition"])
 def test_build_matches_oracle(coracle, m, strategy):
     n = 200_000 if m > 100_000 else 5_000
@@ -171,11 +172,34 @@ def test_clear_resets():
     assert not f.words().any()
 
 
+@pytest.mark.parametrize("strategy", STRATEGIES, ids=["atomic", "lds", "partition"])
+def test_deferred_clear_then_build_and_probe(coracle, strategy):
+    """clear() defers its memset; every later use must still see zeros first."""
+    m = 120_000 if strategy == bh.BUILD_LDS else 10_000_019
+    a, b = rand_keys(300_000, 40), rand_keys(300_000, 41)
+    f = bh.BloomFilter(m)
+    if not supported(f, strategy):
+        pytest.skip("n/a")
+    f.set_batch(a)
+    f.clear()
+    f.set_batch(b)                      # build straight after the deferred clear
+    assert (f.words() == coracle.build(m, b)).all()
+    f.clear()
+    probe = np.concatenate([b[:1000], a[:1000]])
+    got = bh.test_batch([f], probe)[0]  # probe of a cleared filter: all miss
+    assert not got.any()
+    f.clear()
+    f.set_batch(a)
+    f.set_batch(b)                      # second batch merges
+    assert (f.words() == coracle.build(m, np.concatenate([a, b]))).all()
+
+
 # ---------------------------------------------------------------- probe ----
 PROBES = [bh.PROBE_GATHER, bh.PROBE_PARTITION]
 
 
-@pytest.mark.parametrize("m", [1, 64, 65, 1000, 655_360, 1_000_003, 167_772_160, 2**32 + 15])
+@pytest.mark.parametrize("m", [1, 64, 65, 1000, 655_360, 1_000_003, 167_772_160, 671_088_640,
+                               2**32 - 1, 2**32 + 15])
 @pytest.mark.parametrize("probe", PROBES, ids=["gather", "partition"])
 def test_probe_matches_oracle(coracle, m, probe):
     keys = rand_keys(100_000 if m < 2**32 else 20_000, 21)

@@ -37,12 +37,13 @@ def timeit(which, buf, nbytes, m, grid, block, iters, reps=5):
     return a.elapsed_time(b) / reps
 
 
-def part_ablation():
-    """Pass 1 of the partition build on C2 with phases removed."""
+def part_ablation(n=16_777_216, bpe=10.0):
+    """Pass 1 of the partition build (C2 by default) with phases removed, and
+    pass-2 variants on its output."""
     sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
     import bloomhip as bh
-    keys = torch.from_numpy(bh.gen_puts(13141, 16_777_216)).cuda()
-    m = 167_772_160
+    keys = torch.from_numpy(bh.gen_puts(13141, n)).cuda()
+    m = bh.m_bits(n, bpe)
     ntiles = (keys.numel() + 4095) // 4096
     nbins = 4096  # upper bound for the run-start table
     pos = torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda")
@@ -66,11 +67,11 @@ def part_ablation():
     # pass 2 variants on the positions of a full pass 1 (sub-segment order,
     # then segment order)
     words = torch.zeros((m + 63) // 64 * 2, dtype=torch.int32, device="cuda")
-    for layout, ab in (("sub-sorted", 0), ("seg-sorted", 10)):
+    for layout, ab in (("sub-sorted", 0),):
         LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(), rs.data_ptr(),
                             s.cuda_stream)
         torch.cuda.synchronize()
-        for batch in (16, 101, 102):
+        for batch in (16, 200, 101, 102, 16, 200):
             for _ in range(2):
                 LIB.ubench_part_apply(batch, pos.data_ptr(), rs.data_ptr(), keys.numel(), m,
                                       words.data_ptr(), s.cuda_stream)
@@ -92,6 +93,8 @@ def main():
         return isa_rates()
     if len(sys.argv) > 1 and sys.argv[1] == "part":
         return part_ablation()
+    if len(sys.argv) > 1 and sys.argv[1] == "part_c5":
+        return part_ablation(67_108_864, 10.0)
     grid, block = 2048, 256
     threads = grid * block
     out = []
