@@ -146,7 +146,7 @@ struct Workspace {
     std::mutex mu;  // held while work using the buffers is enqueued
     uint32_t *pos = nullptr;  // tile-sorted segment offsets
     size_t pos_bytes = 0;
-    uint32_t *runs = nullptr;  // per-tile run starts
+    uint32_t *runs = nullptr;  // run starts: tile-major rows, then segment-major
     size_t runs_bytes = 0;
     uint8_t *res = nullptr;  // partitioned probe: result byte per sorted entry
     size_t res_bytes = 0;
@@ -273,10 +273,11 @@ int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
     ws.ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->pos), &w->pos_bytes,
                          ws.ntiles * (size_t)kPartTilePos * 4, s));
-    HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->runs), &w->runs_bytes,
-                         ws.ntiles * (ws.nbins + 1) * 4, s));
+    const size_t table = ws.ntiles * (ws.nbins + 1);  // run starts, both layouts
+    HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->runs), &w->runs_bytes, table * 2 * 4, s));
     ws.pos = w->pos;
-    ws.run_starts = w->runs;
+    ws.run_rows = w->runs;
+    ws.run_starts = w->runs + table;
     *out = ws;
     return BLOOMHIP_OK;
 }

@@ -51,15 +51,18 @@ constexpr size_t kPartTileKeys = (size_t)kPartBlock * kPartKPT;  // 4096
 constexpr int kPartTilePos = (int)kPartTileKeys * 3;
 constexpr size_t kPartMaxBins = 4096;  // sub-segments sorted by pass 1
 
-// Probe: filters up to this size are gathered directly (they stay resident in
-// every XCD's 4 MiB L2); larger ones use the partitioned probe when the batch
-// has at least kProbePartitionMinKeys keys.
-constexpr size_t kProbeGatherMaxBytes = 2u << 20;
+// Probe: filters up to this size are gathered directly; larger ones use the
+// partitioned probe when the batch has at least kProbePartitionMinKeys keys.
+// Measured at C3 (16.8M GET keys, tools/probe_sweep.py): gather 134 us vs
+// partition 247 us for the 5 MiB level-3 filter, 531 vs 259 us for the
+// 20 MiB level 4 (gathers then miss the 4 MiB per-XCD L2 on most probes).
+constexpr size_t kProbeGatherMaxBytes = 8u << 20;
 constexpr size_t kProbePartitionMinKeys = 1u << 18;
 
 struct PartitionWorkspace {
     uint32_t *pos;         // [ntiles * kPartTilePos] tile-sorted positions
-    uint32_t *run_starts;  // [ntiles * (nbins + 1)], run starts per pass-2 segment
+    uint32_t *run_rows;    // [ntiles * (nbins + 1)], pass-1 run starts, tile-major
+    uint32_t *run_starts;  // [(nbins + 1) * ntiles], the same segment-major (pass 2)
     size_t ntiles;
     size_t nbins;          // pass-2 segments
     uint32_t sub_shift;    // pass-1 sub-segment = pos >> sub_shift

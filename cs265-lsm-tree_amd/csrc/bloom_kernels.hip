@@ -155,14 +155,39 @@ __device__ __forceinline__ void load_tile_keys(const KeySpan &ks, size_t tile, i
     }
 }
 
+// Bijective block -> work-unit map that gives each XCD a contiguous range of
+// units (cdna_hip_programming.md §5.5 T1, bijective form for n % 8 != 0).
+__device__ __forceinline__ unsigned xcd_remap(unsigned x, unsigned n) {
+    constexpr unsigned kXcds = 8;
+    const unsigned q = n / kXcds, r = n % kXcds;
+    const unsigned xcd = x % kXcds, idx = x / kXcds;
+    // XCD xcd owns units [start, start + q + (xcd < r)).
+    const unsigned start = xcd * q + min(xcd, r);
+    return start + idx;
+}
+
+// Pass-1 tile of persistent block x in round k: each round covers the next
+// gridDim.x tiles, dealt so that every XCD takes a contiguous range of them
+// (segment-major run-start stores then fill whole lines in one L2).  ntiles
+// when the block has no tile in that round.
+__device__ __forceinline__ size_t part_tile(size_t k, size_t ntiles) {
+    const size_t base = k * gridDim.x;
+    if (base >= ntiles) return ntiles;
+    const size_t nr = min((size_t)gridDim.x, ntiles - base);
+    return blockIdx.x < nr ? base + xcd_remap(blockIdx.x, (unsigned)nr) : ntiles;
+}
+
 // ABLATE (timing builds only, tools/ubench): 1 = skip the sorted-tile store,
 // 2 = also skip the LDS scatter, 3 = hash only.  The product launches 0.
-// SEG_SORT (timing builds only): sort by pass-2 segment sub / group instead of
-// by sub-segment (same runs, different order inside a run).
-template <int LAYOUT, int ABLATE = 0, bool SLOTS = false, bool SEG_SORT = false>
+// Outputs: pos_out[tile * kPartTilePos + i], the tile's positions sorted by
+// sub-segment, and where segment b's run of the tile starts (b = 0..nbins):
+// COLS = true: straight into the segment-major table runs[b * ntiles + tile];
+// COLS = false: into the tile-major runs[tile * (nbins + 1) + b], for
+// k_runs_transpose (large tables: see there).
+template <int LAYOUT, int ABLATE = 0, bool SLOTS = false, bool COLS = true>
 __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParams mp,
                                                          uint32_t *__restrict__ pos_out,
-                                                         uint32_t *__restrict__ run_starts,
+                                                         uint32_t *__restrict__ runs,
                                                          int nbins, int nsub, int sub_shift,
                                                          int group, size_t ntiles,
                                                          uint16_t *__restrict__ slots) {
@@ -173,14 +198,16 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     int32_t kcur[kPartKPT], knext[kPartKPT];
-    if (blockIdx.x < ntiles) load_tile_keys<LAYOUT>(ks, blockIdx.x, tid, kcur);
+    size_t tile = part_tile(0, ntiles);
+    if (tile < ntiles) load_tile_keys<LAYOUT>(ks, tile, tid, kcur);
 
-    for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (size_t round = 0; tile < ntiles; round++) {
         const size_t tile0 = tile * kPartTileKeys;
         const int tile_keys = (int)min((size_t)kPartTileKeys, ks.n - tile0);
         for (int b = tid; b <= nsub; b += kPartBlock) s_hist[b] = 0;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
-        if (tile + gridDim.x < ntiles) load_tile_keys<LAYOUT>(ks, tile + gridDim.x, tid, knext);
+        const size_t next = part_tile(round + 1, ntiles);
+        if (next < ntiles) load_tile_keys<LAYOUT>(ks, next, tid, knext);
 
         // 1. positions, and each one's rank inside its sub-segment (LDS
         //    atomics).  br[] keeps (sub-segment << 16) | rank (sub < 4096,
@@ -197,8 +224,7 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
                 if constexpr (ABLATE < 3) {
 #pragma unroll
                     for (int h = 0; h < 3; h++) {
-                        uint32_t sub = pos[3 * j + h] >> sub_shift;
-                        if constexpr (SEG_SORT) sub = (sub / (uint32_t)group) * (uint32_t)group;
+                        const uint32_t sub = pos[3 * j + h] >> sub_shift;
                         br[3 * j + h] = (sub << 16) | atomicAdd(&s_hist[sub], 1u);
                     }
                 }
@@ -211,6 +237,7 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
             if (acc == 0x9E3779B9u) pos_out[tid] = acc;
 #pragma unroll
             for (int j = 0; j < kPartKPT; j++) kcur[j] = knext[j];
+            tile = next;
             continue;
         }
         lds_barrier();
@@ -245,9 +272,14 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
             }
         }
         lds_barrier();
-        uint32_t *row = run_starts + tile * (size_t)(nbins + 1);
-        for (int b = tid; b <= nbins; b += kPartBlock)
-            row[b] = s_hist[b == nbins ? nsub : b * group];
+        if constexpr (COLS) {
+            for (int b = tid; b <= nbins; b += kPartBlock)
+                runs[(size_t)b * ntiles + tile] = s_hist[b == nbins ? nsub : b * group];
+        } else {
+            uint32_t *row = runs + tile * (size_t)(nbins + 1);
+            for (int b = tid; b <= nbins; b += kPartBlock)
+                row[b] = s_hist[b == nbins ? nsub : b * group];
+        }
 
         if constexpr (ABLATE < 2) {
             // 3. scatter into the LDS image sorted by segment.
@@ -276,11 +308,46 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
             for (int q = tid; q < nq; q += kPartBlock)
                 reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(s_sorted)[q];
             for (int e = nq * 4 + tid; e < npos; e += kPartBlock) dst[e] = s_sorted[e];
+            // the short last tile: pad with a position no segment holds, since
+            // pass 2 reads whole 16-B vectors and past run ends
+            for (int e = npos + tid; e < kPartTilePos; e += kPartBlock) dst[e] = 0xFFFFFFFFu;
         } else if constexpr (ABLATE == 1) {
             if (s_sorted[tid] == 0xFFFFFFFFu) pos_out[tid] = 0;
         }
 #pragma unroll
         for (int j = 0; j < kPartKPT; j++) kcur[j] = knext[j];
+        tile = next;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// run-start transpose: pass 1 writes one row of nbins + 1 run starts per tile
+// (contiguous, cheap); pass 2 wants, per segment, its run bounds of all tiles
+// contiguous.  A 64 x 64 LDS-tiled transpose: 256-B coalesced reads and
+// writes, the LDS tile padded one word per row against bank conflicts.
+// Small tables are written straight from pass 1 as columns (COLS): at C2
+// (4 MiB) that costs ~2 us against ~6 us for a transpose launch.  Large ones
+// go through the transpose: at C4 (805 MB) the column stores cost ~2.1 ms
+// (partial-line write-backs), the transpose 0.39 ms (tools/ubench.py part*).
+// ---------------------------------------------------------------------------
+constexpr size_t kColumnTableMaxBytes = 128u << 20;
+constexpr int kTransposeTile = 64;
+constexpr int kTransposeBlock = 256;
+
+__global__ void __launch_bounds__(kTransposeBlock) k_runs_transpose(
+    const uint32_t *__restrict__ rows, uint32_t *__restrict__ cols, size_t ntiles, int width) {
+    __shared__ uint32_t t[kTransposeTile][kTransposeTile + 1];
+    const int b0 = blockIdx.x * kTransposeTile;           // first segment column
+    const size_t t0 = (size_t)blockIdx.y * kTransposeTile;  // first tile row
+    const int x = threadIdx.x & 63, y0 = threadIdx.x >> 6;
+    for (int y = y0; y < kTransposeTile; y += kTransposeBlock / 64) {
+        const size_t tile = t0 + y;
+        if (tile < ntiles && b0 + x < width) t[y][x] = rows[tile * width + b0 + x];
+    }
+    __syncthreads();
+    for (int y = y0; y < kTransposeTile; y += kTransposeBlock / 64) {
+        const size_t tile = t0 + x;
+        if (tile < ntiles && b0 + y < width) cols[(size_t)(b0 + y) * ntiles + tile] = t[x][y];
     }
 }
 
@@ -291,62 +358,64 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
 // non-zero).  Segments never overlap, so no atomics leave the CU.
 // ---------------------------------------------------------------------------
 
-// Bijective block -> work-unit map that gives each XCD a contiguous range of
-// units (cdna_hip_programming.md §5.5 T1, bijective form for n % 8 != 0).
-__device__ __forceinline__ unsigned xcd_remap(unsigned x, unsigned n) {
-    constexpr unsigned kXcds = 8;
-    const unsigned q = n / kXcds, r = n % kXcds;
-    const unsigned xcd = x % kXcds, idx = x / kXcds;
-    // XCD xcd owns units [start, start + q + (xcd < r)).
-    const unsigned start = xcd * q + min(xcd, r);
-    return start + idx;
-}
 constexpr int kApplyBlock = 1024;
 constexpr int kApplyWaves = kApplyBlock / 64;
-constexpr int kApplyChunk = kApplyBlock;  // tiles whose run bounds are staged in LDS at once
-constexpr int kApplyBatch = 16;           // runs per batch; two batches in flight
-// At >= this many segments a tile's runs average <= 64 entries (12288/192);
-// at >= kFlatRunBins they average <= 24 and are walked flattened.
-constexpr size_t kShortRunBins = 192;
-constexpr size_t kFlatRunBins = 512;
-constexpr int kFlatDepth = 16;  // 64-entry loads a wave has in flight
-constexpr int kRunsShort = 0, kRunsLong = 1, kRunsFlat = 2;
-static_assert(kApplyChunk == kApplyWaves * 64, "one 64-tile slice per wave per chunk");
+constexpr int kApplyDepth = 4;  // lane-group loads per wave per batch
+
+// Lanes per tile for pass 2, from the average run length L = kPartTilePos /
+// nbins.  A step of 4G entries per tile; runs longer than a step finish in
+// the wave-uniform tail loop.  Measured on MI355X (tools/ubench.py part*):
+// G = 8 beats G = 16 even at L = 48 (C2), G = 4 ~ G = 8 at L = 4 (C4), G = 2
+// is always worse (its loads cover too few bytes per lane group).
+inline int apply_lanes_per_tile(size_t nbins) {
+    const size_t L = kPartTilePos / (nbins ? nbins : 1);
+    if (L < 10) return 4;
+    if (L < 96) return 8;
+    if (L < 192) return 16;
+    return 32;
+}
 
 // PROBE = false: build (OR every entry into the zeroed LDS image, write the
 // segment).  PROBE = true: the LDS image is the filter's segment; each entry's
 // bit is written as one result byte at the entry's own index in the sorted
 // tile (res[tile*kPartTilePos + index]), so the result stores follow the runs
 // and coalesce like the loads.
-// RUNS selects how a wave walks its tiles' runs:
-//   kRunsShort: runs rarely exceed 64 entries: one load per run, BATCH runs
-//               per step, the rare longer run finishes in a per-tile tail.
-//   kRunsLong:  few segments, runs span several 64-entry steps; the wave
-//               walks (batch, offset) steps.
-//   kRunsFlat:  many segments, runs much shorter than 64 entries: the wave
-//               concatenates its 64 tiles' runs and walks them 64 entries per
-//               load, each lane finding its tile by binary search over the
-//               run prefix sums held one per lane (ds_bpermute).
-// ABLATE (timing builds only): 1 = skip the LDS ORs, 2 = skip the position
-// loads (synthetic entries).  The product launches 0.
-template <bool PROBE, int RUNS, int BATCH = kApplyBatch, int ABLATE = 0>
+//
+// The walk: G consecutive lanes share one tile and read its run as 16-B
+// vectors, lane j of the group starting at the run's 16-B-aligned start
+// + 4j, so one load instruction covers 64/G tiles x 4G entries.  The lanes
+// never test run bounds per entry: the sorted tile holds segment b's run
+// between runs of segments < b and > b, so an entry belongs to this segment
+// exactly when (position - base) < lim.  Reading past either end of the run
+// therefore only loads other segments' entries (the last tile's tail is
+// padded with 0xFFFFFFFF by pass 1), and lanes of tiles past the end re-read
+// the last tile, which ORs / writes the same values twice.  A wave owns
+// batches of kApplyDepth load groups; the next batch's run bounds are loaded
+// while the current one is applied, and the rare tile whose run outlasts the
+// first step is finished by a wave-uniform loop.
+// ABLATE (timing builds only): 1 = skip the LDS ORs.  The product launches 0.
+template <bool PROBE, int G, int ABLATE = 0>
 __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
     const uint32_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
-    int nbins, uint32_t seg_bits, uint32_t *__restrict__ words, uint64_t nw32,
+    int nbins, uint32_t seg_bits, uint64_t m, uint32_t *__restrict__ words, uint64_t nw32,
     int merge_existing, uint8_t *__restrict__ res) {
+    static_assert(G >= 1 && G <= 64 && (64 % G) == 0, "G lanes per tile");
+    constexpr int kTPI = 64 / G;                     // tiles per load instruction
+    constexpr int kBatchTiles = kTPI * kApplyDepth;  // tiles per wave batch
+    constexpr uint32_t kStep = 4 * G;                // entries a tile advances per step
+    constexpr uint32_t kLastVec = kPartTilePos - 4;
+
     const uint32_t seg_words = seg_bits / 32;
     extern __shared__ __attribute__((aligned(16))) uint32_t seg[];
-    __shared__ uint2 s_run[kApplyChunk];  // (start, end) of this segment's run per tile
-    // Neighbouring segments' runs share 128-B lines of every sorted tile, so
-    // give consecutive segments to workgroups on one XCD (blocks are dealt
-    // round-robin over the 8 XCDs): a bijection on [0, nbins); placement only
-    // affects speed.
+    // Neighbouring segments' runs share 128-B lines of every sorted tile and
+    // of the run-start rows, so give consecutive segments to workgroups on one
+    // XCD (blocks are dealt round-robin over the 8 XCDs): a bijection on
+    // [0, nbins); placement only affects speed.
     const int b = (int)xcd_remap(blockIdx.x, (unsigned)nbins);
-    const int t_begin = 0;
-    const int t_end = ntiles;
     const uint64_t w0 = (uint64_t)b * seg_words;
     const int nseg = (int)(min(nw32, w0 + seg_words) - w0);  // last segment may be short
     const uint32_t base = (uint32_t)b * seg_bits;             // entries are full positions
+    const uint32_t lim = (uint32_t)min((uint64_t)seg_bits, m - base);
     if constexpr (PROBE) {
         for (int i = threadIdx.x; i < (int)seg_words; i += kApplyBlock)
             seg[i] = i < nseg ? words[w0 + i] : 0u;
@@ -354,161 +423,98 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
         for (int i = threadIdx.x; i < (int)seg_words / 4; i += kApplyBlock)
             reinterpret_cast<uint4 *>(seg)[i] = make_uint4(0, 0, 0, 0);
     }
+    __syncthreads();
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const size_t stride = (size_t)nbins + 1;
-    // Run bounds of tile t for segment b, fetched one chunk ahead.
-    auto fetch_run = [&](int t) -> uint2 {
-        if (t >= t_end) return make_uint2(0, 0);
-        const uint32_t *row = run_starts + (size_t)t * stride + b;
-        return make_uint2(row[0], row[1]);
-    };
-    uint2 r_next = fetch_run(t_begin + (int)threadIdx.x);
-    for (int c0 = t_begin; c0 < t_end; c0 += kApplyChunk) {
-        __syncthreads();  // previous chunk's s_run fully consumed (and seg zeroed)
-        s_run[threadIdx.x] = r_next;
-        __syncthreads();
-        r_next = fetch_run(c0 + kApplyChunk + (int)threadIdx.x);
-        // wave w owns tiles c0 + 64w .. c0 + 64w + 63 of this chunk; its runs
-        // are read BATCH at a time, the next batch's loads issued before
-        // the current batch's LDS ORs.
-        const int wt0 = wave * 64;
-        const int wtn = max(0, min(64, t_end - (c0 + wt0)));
-        const uint32_t *wbase = pos + (size_t)(c0 + wt0) * kPartTilePos;
-        // The wave's work is a sequence of steps (k0, off): entries
-        // [off, off + 64) of the runs of tiles k0 .. k0 + BATCH - 1.
-        // Loads of the next step are issued before the current step's LDS
-        // work, so two steps (2 * BATCH loads per lane) are in flight.
-        uint32_t cur[BATCH], nxt[BATCH];
-        auto batch_maxlen = [&](int k0) -> uint32_t {
-            uint32_t ml = 0;
+    const uint32_t sub4 = (uint32_t)(lane % G) * 4;  // this lane's offset in its tile's step
+    const int tl = lane / G;                         // this lane's tile in a load group
+    const int nbatch = (ntiles + kBatchTiles - 1) / kBatchTiles;
+
+    auto bounds = [&](int j, uint2 (&r)[kApplyDepth]) {
 #pragma unroll
-            for (int k = 0; k < BATCH; k++) {
-                if (k0 + k < wtn) {
-                    const uint2 r = s_run[wt0 + k0 + k];
-                    ml = max(ml, r.y - r.x);
-                }
-            }
-            return __builtin_amdgcn_readfirstlane(ml);
-        };
-        auto load_step = [&](int k0, uint32_t off, uint32_t (&v)[BATCH]) {
-#pragma unroll
-            for (int k = 0; k < BATCH; k++) {
-                const uint2 r = k0 + k < wtn ? s_run[wt0 + k0 + k] : make_uint2(0, 0);
-                const uint32_t e = r.x + off + lane;
-                if constexpr (ABLATE == 2)
-                    v[k] = e < r.y ? ((e * 2654435761u) >> 13) % 524288u : 0xFFFFFFFFu;
-                else
-                    // raw position; `base` is subtracted where it is consumed,
-                    // so the load stays in flight until apply_step
-                    v[k] = e < r.y ? wbase[(size_t)(k0 + k) * kPartTilePos + e] : 0xFFFFFFFFu;
-            }
-        };
-        auto apply_step = [&](int k0, uint32_t off, const uint32_t (&v)[BATCH]) {
-#pragma unroll
-            for (int k = 0; k < BATCH; k++) {
-                if (v[k] == 0xFFFFFFFFu) continue;
-                const uint32_t o = v[k] - (ABLATE == 2 ? 0u : base);
-                if constexpr (PROBE) {
-                    const uint32_t e = s_run[wt0 + k0 + k].x + off + lane;
-                    res[(size_t)(c0 + wt0 + k0 + k) * kPartTilePos + e] =
-                        (seg[o >> 5] >> (o & 31)) & 1u;
-                } else if constexpr (ABLATE == 1) {
-                    (void)off;
-                    asm volatile("" ::"v"(o));
-                } else {
-                    (void)off;
-                    atomicOr(&seg[o >> 5], 1u << (o & 31));
-                }
-            }
-        };
-        if (wtn <= 0) continue;
-        if constexpr (RUNS == kRunsFlat) {
-            // lane t: tile t's run length L, its exclusive prefix P and the
-            // offset O mapping a concatenated index e to wbase[e + O].
-            uint32_t L = 0, O = 0;
-            if (lane < wtn) {
-                const uint2 r = s_run[wt0 + lane];
-                L = r.y - r.x;
-                O = (uint32_t)lane * kPartTilePos + r.x;
-            }
-            uint32_t incl = L;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t t = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += t;
-            }
-            const uint32_t P = incl - L;
-            O -= P;
-            const uint32_t T = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
-            for (uint32_t s0 = 0; s0 < T; s0 += 64 * kFlatDepth) {
-                uint32_t v[kFlatDepth], idx[kFlatDepth];
-#pragma unroll
-                for (int d = 0; d < kFlatDepth; d++) {
-                    const uint32_t e = s0 + (uint32_t)d * 64 + lane;
-                    int lo = 0;  // largest tile with P <= e (P is non-decreasing)
-#pragma unroll
-                    for (int st = 32; st >= 1; st >>= 1) {
-                        const uint32_t pc = __shfl(P, lo + st, 64);
-                        if (pc <= e) lo += st;
-                    }
-                    idx[d] = e + __shfl(O, lo, 64);
-                    v[d] = e < T ? wbase[idx[d]] : 0xFFFFFFFFu;
-                }
-#pragma unroll
-                for (int d = 0; d < kFlatDepth; d++) {
-                    if (v[d] == 0xFFFFFFFFu) continue;
-                    const uint32_t o = v[d] - base;
-                    if constexpr (PROBE)
-                        res[(size_t)(c0 + wt0) * kPartTilePos + idx[d]] = (seg[o >> 5] >> (o & 31)) & 1u;
-                    else
-                        atomicOr(&seg[o >> 5], 1u << (o & 31));
-                }
-            }
-        } else if constexpr (RUNS == kRunsLong) {
-            int k0 = 0;
-            uint32_t off = 0, ml = batch_maxlen(0);
-            load_step(k0, off, cur);
-            while (true) {
-                int nk0 = k0;
-                uint32_t noff = off + 64, nml = ml;
-                if (noff >= ml) {
-                    nk0 = k0 + BATCH;
-                    noff = 0;
-                    nml = nk0 < wtn ? batch_maxlen(nk0) : 0;
-                }
-                const bool more = nk0 < wtn;
-                if (more) load_step(nk0, noff, nxt);
-                apply_step(k0, off, cur);
-                if (!more) break;
-#pragma unroll
-                for (int k = 0; k < BATCH; k++) cur[k] = nxt[k];
-                k0 = nk0;
-                off = noff;
-                ml = nml;
-            }
-        } else {
-            load_step(0, 0, cur);
-            for (int k0 = 0; k0 < wtn; k0 += BATCH) {
-                if (k0 + BATCH < wtn) load_step(k0 + BATCH, 0, nxt);
-                apply_step(k0, 0, cur);
-#pragma unroll
-                for (int k = 0; k < BATCH; k++) cur[k] = nxt[k];
-            }
-            for (int k = 0; k < wtn; k++) {  // entries past the first 64 of a run
-                const uint2 r = s_run[wt0 + k];
-                for (uint32_t e = r.x + 64 + lane; e < r.y; e += 64) {
-                    const uint32_t v = wbase[(size_t)k * kPartTilePos + e] - base;
-                    if constexpr (PROBE) {
-                        res[(size_t)(c0 + wt0 + k) * kPartTilePos + e] =
-                            (seg[v >> 5] >> (v & 31)) & 1u;
-                    } else {
-                        atomicOr(&seg[v >> 5], 1u << (v & 31));
-                    }
-                }
+        for (int d = 0; d < kApplyDepth; d++) {
+            const int t = j * kBatchTiles + d * kTPI + tl;
+            if (t < ntiles) {
+                r[d] = make_uint2(run_starts[(size_t)b * ntiles + t],
+                                  run_starts[(size_t)(b + 1) * ntiles + t]);
+            } else {
+                r[d] = make_uint2(0, 0);
             }
         }
+    };
+    auto load = [&](int t, uint32_t e) -> uint4 {
+        return *reinterpret_cast<const uint4 *>(pos + (size_t)t * kPartTilePos + e);
+    };
+    auto apply1 = [&](uint32_t v, int t, uint32_t e) {
+        const uint32_t o = v - base;
+        if constexpr (ABLATE == 1) {
+            asm volatile("" ::"v"(o));
+            (void)t; (void)e;
+        } else if (o < lim) {
+            if constexpr (PROBE) {
+                res[(size_t)t * kPartTilePos + e] = (seg[o >> 5] >> (o & 31)) & 1u;
+            } else {
+                (void)t; (void)e;
+                atomicOr(&seg[o >> 5], 1u << (o & 31));
+            }
+        }
+    };
+    auto apply4 = [&](const uint4 &v, int t, uint32_t e) {
+        if constexpr (PROBE && ABLATE == 0) {
+            // the 4 result bytes go out as one dword when all 4 entries are
+            // this segment's (inside a run), else byte by byte
+            const uint32_t o[4] = {v.x - base, v.y - base, v.z - base, v.w - base};
+            uint32_t bits = 0, mask = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (o[k] < lim) {
+                    mask |= 1u << k;
+                    bits |= ((seg[o[k] >> 5] >> (o[k] & 31)) & 1u) << (8 * k);
+                }
+            }
+            uint8_t *p = res + (size_t)t * kPartTilePos + e;
+            if (mask == 0xFu) {
+                *reinterpret_cast<uint32_t *>(p) = bits;
+            } else if (mask != 0) {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (mask & (1u << k)) p[k] = (uint8_t)(bits >> (8 * k));
+            }
+        } else {
+            apply1(v.x, t, e);
+            apply1(v.y, t, e + 1);
+            apply1(v.z, t, e + 2);
+            apply1(v.w, t, e + 3);
+        }
+    };
+
+    uint2 r[kApplyDepth];
+    if (wave < nbatch) bounds(wave, r);
+    for (int j = wave; j < nbatch; j += kApplyWaves) {
+        int t[kApplyDepth];
+        uint32_t e[kApplyDepth];
+        uint4 v[kApplyDepth];
+#pragma unroll
+        for (int d = 0; d < kApplyDepth; d++) {
+            t[d] = min(j * kBatchTiles + d * kTPI + tl, ntiles - 1);
+            e[d] = (r[d].x & ~3u) + sub4;
+            v[d] = load(t[d], min(e[d], kLastVec));
+        }
+        uint2 rn[kApplyDepth];
+        const int jn = j + kApplyWaves;
+        if (jn < nbatch) bounds(jn, rn);
+#pragma unroll
+        for (int d = 0; d < kApplyDepth; d++) apply4(v[d], t[d], min(e[d], kLastVec));
+#pragma unroll
+        for (int d = 0; d < kApplyDepth; d++) {
+            for (uint32_t en = e[d] + kStep; __ballot(en < r[d].y) != 0; en += kStep) {
+                const uint32_t ec = min(en, kLastVec);
+                apply4(load(t[d], ec), t[d], ec);
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < kApplyDepth; d++) r[d] = rn[d];
     }
     if constexpr (PROBE) return;
     __syncthreads();
@@ -718,69 +724,96 @@ bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
     return true;
 }
 
+hipError_t launch_runs_transpose(const PartitionWorkspace &ws, hipStream_t stream) {
+    const int width = (int)ws.nbins + 1;
+    const dim3 grid((unsigned)((width + kTransposeTile - 1) / kTransposeTile),
+                    (unsigned)((ws.ntiles + kTransposeTile - 1) / kTransposeTile));
+    if (grid.y > 65535u) return hipErrorInvalidValue;  // > 2^28 keys per batch
+    k_runs_transpose<<<grid, kTransposeBlock, 0, stream>>>(ws.run_rows, ws.run_starts, ws.ntiles,
+                                                           width);
+    return hipGetLastError();
+}
+
+bool runs_as_columns(const PartitionWorkspace &ws) {
+    return ws.ntiles * (ws.nbins + 1) * 4 <= kColumnTableMaxBytes;
+}
+
+// Pass 1 for a build (SLOTS = false) or a probe (SLOTS = true), then the
+// run-start transpose when the table is large.
+template <bool SLOTS>
+hipError_t launch_bin(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                      uint16_t *slots, hipStream_t stream) {
+    const unsigned grid = part_bin_grid(ws.ntiles);
+    const bool cols = runs_as_columns(ws);
+    uint32_t *runs = cols ? ws.run_starts : ws.run_rows;
+    const int nb = (int)ws.nbins, ns = (int)ws.nsub, sh = (int)ws.sub_shift, g = (int)ws.group;
+#define BIN_LAUNCH(L, C)                                                                     \
+    k_part_bin<L, 0, SLOTS, C><<<grid, kPartBlock, 0, stream>>>(ks, mp, ws.pos, runs, nb, ns, sh, \
+                                                               g, ws.ntiles, slots)
+    if (ks.layout == KEYS_PACKED) {
+        if (cols) BIN_LAUNCH(KEYS_PACKED, true); else BIN_LAUNCH(KEYS_PACKED, false);
+    } else {
+        if (cols) BIN_LAUNCH(KEYS_STRIDED, true); else BIN_LAUNCH(KEYS_STRIDED, false);
+    }
+#undef BIN_LAUNCH
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess || cols) return e;
+    return launch_runs_transpose(ws, stream);
+}
+
 hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                            hipStream_t stream) {
     if (ks.n == 0) return hipSuccess;
-    const unsigned grid = part_bin_grid(ws.ntiles);
-    if (ks.layout == KEYS_PACKED)
-        k_part_bin<KEYS_PACKED><<<grid, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, (int)ws.nsub, (int)ws.sub_shift,
-            (int)ws.group, ws.ntiles, nullptr);
-    else
-        k_part_bin<KEYS_STRIDED><<<grid, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, (int)ws.nsub, (int)ws.sub_shift,
-            (int)ws.group, ws.ntiles, nullptr);
-    return hipGetLastError();
+    return launch_bin<false>(ks, mp, ws, nullptr, stream);
 }
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
-template <bool PROBE, int RUNS>
-hipError_t launch_apply(const PartitionWorkspace &ws, uint32_t *words, uint64_t nw32, int merge,
-                        uint8_t *res, hipStream_t stream) {
+template <bool PROBE, int G>
+hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
+                          uint64_t nw32, int merge, uint8_t *res, hipStream_t stream) {
     static const bool attr_set = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<PROBE, RUNS>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<PROBE, G>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kSegMaxBits / 8));
         return true;
     }();
     (void)attr_set;
-    k_part_apply<PROBE, RUNS><<<(unsigned)ws.nbins, kApplyBlock, ws.seg_bits / 8, stream>>>(
-        ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, words, nw32, merge, res);
+    k_part_apply<PROBE, G><<<(unsigned)ws.nbins, kApplyBlock, ws.seg_bits / 8, stream>>>(
+        ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
+        res);
     return hipGetLastError();
+}
+
+template <bool PROBE>
+hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *words, uint64_t nw32,
+                        int merge, uint8_t *res, hipStream_t stream) {
+    switch (apply_lanes_per_tile(ws.nbins)) {
+        case 2: return launch_apply_g<PROBE, 2>(ws, m, words, nw32, merge, res, stream);
+        case 4: return launch_apply_g<PROBE, 4>(ws, m, words, nw32, merge, res, stream);
+        case 8: return launch_apply_g<PROBE, 8>(ws, m, words, nw32, merge, res, stream);
+        case 16: return launch_apply_g<PROBE, 16>(ws, m, words, nw32, merge, res, stream);
+        case 32: return launch_apply_g<PROBE, 32>(ws, m, words, nw32, merge, res, stream);
+        default: return launch_apply_g<PROBE, 64>(ws, m, words, nw32, merge, res, stream);
+    }
 }
 
 hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const PartitionWorkspace &ws,
                              int merge_existing, hipStream_t stream) {
     if (ws.ntiles == 0) return hipSuccess;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
-    if (ws.nbins >= kFlatRunBins)
-        return launch_apply<false, kRunsFlat>(ws, words, nw32, merge_existing, nullptr, stream);
-    if (ws.nbins >= kShortRunBins)
-        return launch_apply<false, kRunsShort>(ws, words, nw32, merge_existing, nullptr, stream);
-    return launch_apply<false, kRunsLong>(ws, words, nw32, merge_existing, nullptr, stream);
+    return launch_apply<false>(ws, mp.m, words, nw32, merge_existing, nullptr, stream);
 }
 
 hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, const uint32_t *words,
                                     const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
                                     uint64_t *out, hipStream_t stream) {
     if (ks.n == 0) return hipSuccess;
-    const unsigned g1 = part_bin_grid(ws.ntiles);
-    if (ks.layout == KEYS_PACKED)
-        k_part_bin<KEYS_PACKED, 0, true><<<g1, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, (int)ws.nsub, (int)ws.sub_shift,
-            (int)ws.group, ws.ntiles, slots);
-    else
-        k_part_bin<KEYS_STRIDED, 0, true><<<g1, kPartBlock, 0, stream>>>(
-            ks, mp, ws.pos, ws.run_starts, (int)ws.nbins, (int)ws.nsub, (int)ws.sub_shift,
-            (int)ws.group, ws.ntiles, slots);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_bin<true>(ks, mp, ws, slots, stream);
     if (e != hipSuccess) return e;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
     uint32_t *w = const_cast<uint32_t *>(words);  // read-only in PROBE mode
-    e = ws.nbins >= kFlatRunBins    ? launch_apply<true, kRunsFlat>(ws, w, nw32, 0, res, stream)
-        : ws.nbins >= kShortRunBins ? launch_apply<true, kRunsShort>(ws, w, nw32, 0, res, stream)
-                                    : launch_apply<true, kRunsLong>(ws, w, nw32, 0, res, stream);
+    e = launch_apply<true>(ws, mp.m, w, nw32, 0, res, stream);
     if (e != hipSuccess) return e;
     k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out);
     return hipGetLastError();

@@ -104,7 +104,9 @@ extern "C" int ubench_run(int which, void *dbuf, size_t bytes, uint64_t m, int g
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-// Pass 1 of the partition build with phases removed (ABLATE 0..3).
+// Pass 1 of the partition build: 0 = the product's launch, 1..3 = pass 1
+// with phases removed (ABLATE), 4 = pass 1 writing run-start columns, 5 =
+// pass 1 writing rows, 6 = the row -> column transpose alone.
 extern "C" int ubench_part_bin(int ablate, const void *keys, size_t n, uint64_t m, uint32_t *pos,
                                uint32_t *run_starts, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -116,19 +118,30 @@ extern "C" int ubench_part_bin(int ablate, const void *keys, size_t n, uint64_t 
     const size_t ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
     const unsigned grid = part_bin_grid(ntiles);
     const int nsub = (int)ws.nsub, ssh = (int)ws.sub_shift, grp = (int)ws.group;
+    // run_starts holds both layouts: segment-major first, the pass-1 rows after
+    ws.ntiles = ntiles;
+    ws.run_starts = run_starts;
+    ws.run_rows = run_starts + ntiles * (ws.nbins + 1);
+    uint32_t *rows = ws.run_rows;
     switch (ablate) {
-        case 0: k_part_bin<KEYS_PACKED, 0><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 1: k_part_bin<KEYS_PACKED, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 2: k_part_bin<KEYS_PACKED, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 3: k_part_bin<KEYS_PACKED, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 10: k_part_bin<KEYS_PACKED, 0, false, true><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 0:
+            ws.pos = pos;
+            if (launch_part_bin(ks, mp, ws, s) != hipSuccess) return -5;
+            break;
+        case 1: k_part_bin<KEYS_PACKED, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, rows, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 2: k_part_bin<KEYS_PACKED, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, rows, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 3: k_part_bin<KEYS_PACKED, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, rows, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 4: k_part_bin<KEYS_PACKED, 0, false, true><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 5: k_part_bin<KEYS_PACKED, 0, false, false><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, rows, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 6: if (launch_runs_transpose(ws, s) != hipSuccess) return -5; break;
         default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-// Pass 2 of the partition build (variants: 16 = product, 101 = loads only,
-// 102 = LDS only), on the positions of ubench_part_bin ablate 0.
+// Pass 2 of the partition build on the positions of ubench_part_bin ablate 0:
+// variant G in {2..64} = the product walk with G lanes per tile, 100 + G =
+// the same with the LDS ORs skipped (loads only), 0 = the product's choice.
 extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_t *run_starts,
                                  size_t n, uint64_t m, uint32_t *words, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -138,28 +151,27 @@ extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_
     const int ntiles = (int)((n + kPartTileKeys - 1) / kPartTileKeys);
     const uint64_t nw32 = ((m + 63) / 64) * 2;
     const uint32_t sb = ws.seg_bits;
-#define UB_APPLY(B, A)                                                                        \
+    if (variant == 0) variant = apply_lanes_per_tile(ws.nbins);
+#define UB_APPLY(G, A)                                                                        \
     do {                                                                                      \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<false, kRunsShort, B, A>), \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<false, G, A>), \
                                   hipFuncAttributeMaxDynamicSharedMemorySize,                 \
                                   (int)(kSegMaxBits / 8));                                    \
-        k_part_apply<false, kRunsShort, B, A><<<nbins, kApplyBlock, sb / 8, s>>>(                  \
-            pos, run_starts, ntiles, nbins, sb, words, nw32, 0, nullptr);                     \
+        k_part_apply<false, G, A><<<nbins, kApplyBlock, sb / 8, s>>>(                         \
+            pos, run_starts, ntiles, nbins, sb, m, words, nw32, 0, nullptr);                  \
     } while (0)
     switch (variant) {
+        case 2: UB_APPLY(2, 0); break;
+        case 4: UB_APPLY(4, 0); break;
         case 8: UB_APPLY(8, 0); break;
         case 16: UB_APPLY(16, 0); break;
-        case 24: UB_APPLY(24, 0); break;
         case 32: UB_APPLY(32, 0); break;
-        case 48: UB_APPLY(48, 0); break;
-        case 200:  // flattened walk
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<false, kRunsFlat>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kSegMaxBits / 8));
-            k_part_apply<false, kRunsFlat><<<nbins, kApplyBlock, sb / 8, s>>>(
-                pos, run_starts, ntiles, nbins, sb, words, nw32, 0, nullptr);
-            break;
-        case 101: UB_APPLY(16, 1); break;
-        case 102: UB_APPLY(16, 2); break;
+        case 64: UB_APPLY(64, 0); break;
+        case 102: UB_APPLY(2, 1); break;
+        case 104: UB_APPLY(4, 1); break;
+        case 108: UB_APPLY(8, 1); break;
+        case 116: UB_APPLY(16, 1); break;
+        case 132: UB_APPLY(32, 1); break;
         default: return -22;
     }
 #undef UB_APPLY

@@ -47,10 +47,11 @@ def part_ablation(n=16_777_216, bpe=10.0):
     ntiles = (keys.numel() + 4095) // 4096
     nbins = 4096  # upper bound for the run-start table
     pos = torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda")
-    rs = torch.empty(ntiles * (nbins + 1), dtype=torch.int32, device="cuda")
+    rs = torch.empty(ntiles * (nbins + 1) * 2, dtype=torch.int32, device="cuda")  # both layouts
     s = torch.cuda.current_stream()
-    names = {0: "full", 1: "no tile store", 2: "no scatter/store", 3: "hash only"}
-    for ab in range(4):
+    names = {0: "product", 1: "no tile store", 2: "no scatter/store", 3: "hash only",
+             4: "full, column runs", 5: "full, row runs", 6: "transpose only"}
+    for ab in range(7):
         for _ in range(3):
             LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(),
                                 rs.data_ptr(), s.cuda_stream)
@@ -71,10 +72,11 @@ def part_ablation(n=16_777_216, bpe=10.0):
         LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(), rs.data_ptr(),
                             s.cuda_stream)
         torch.cuda.synchronize()
-        for batch in (16, 200, 101, 102, 16, 200):
+        for batch in (0, 2, 4, 8, 16, 32, 104, 108, 116, 0):
             for _ in range(2):
-                LIB.ubench_part_apply(batch, pos.data_ptr(), rs.data_ptr(), keys.numel(), m,
-                                      words.data_ptr(), s.cuda_stream)
+                rc = LIB.ubench_part_apply(batch, pos.data_ptr(), rs.data_ptr(), keys.numel(), m,
+                                           words.data_ptr(), s.cuda_stream)
+                assert rc == 0, (batch, rc)
             torch.cuda.synchronize()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
@@ -83,7 +85,7 @@ def part_ablation(n=16_777_216, bpe=10.0):
                                       words.data_ptr(), s.cuda_stream)
             b.record(s)
             torch.cuda.synchronize()
-            print(json.dumps({"op": "k_part_apply", "layout": layout, "variant": batch,
+            print(json.dumps({"op": "k_part_apply", "n": n, "variant": batch,
                               "us": round(a.elapsed_time(b) / 10 * 1e3, 2)}), flush=True)
 
 
@@ -95,6 +97,8 @@ def main():
         return part_ablation()
     if len(sys.argv) > 1 and sys.argv[1] == "part_c5":
         return part_ablation(67_108_864, 10.0)
+    if len(sys.argv) > 1 and sys.argv[1] == "part_c4":
+        return part_ablation(268_435_456, 12.0)
     grid, block = 2048, 256
     threads = grid * block
     out = []
