@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""HBM bytes per build from two rocprofv3 PMC passes (tools/gpu_prof.sh):
+FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE is doubled (the gfx950
+correction of MI355X_MICROARCH.md, HBM section: it tallies 128-B requests at
+64 B).  Per kernel, the median over the dispatches of its largest grid (the
+workload's own build; smaller grids are the tests' warm-up builds).
+
+Usage: pmc_traffic.py WORKLOAD TAG  -> profiles/pmc_WORKLOAD.json
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import pmc_summary  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD_KERNELS = ("k_part_bin", "k_runs_transpose", "k_part_apply", "k_build_lds",
+                 "k_build_atomic")
+
+
+def per_kernel(d):
+    best = {}
+    for key, ctrs in pmc_summary.main(d).items():
+        name, grid = key.rsplit(" grid=", 1)
+        base = name.split("<")[0]
+        if base not in BUILD_KERNELS or "<true" in name:  # PROBE / SLOTS variants
+            continue
+        if base not in best or int(grid) > best[base][0]:
+            best[base] = (int(grid), name, ctrs)
+    return best
+
+
+def main(w, tag):
+    f = per_kernel(os.path.join(ROOT, "gpurun_out", f"pmc_{w}_{tag}_FETCH_SIZE"))
+    wr = per_kernel(os.path.join(ROOT, "gpurun_out", f"pmc_{w}_{tag}_WRITE_SIZE"))
+    kernels = {}
+    total = 0
+    for base in BUILD_KERNELS:
+        if base not in f or base not in wr:
+            continue
+        fetch = 2 * f[base][2]["FETCH_SIZE"] * 1024
+        write = wr[base][2]["WRITE_SIZE"] * 1024
+        kernels[base] = {"name": f[base][1], "grid": f[base][0], "fetch_bytes": int(fetch),
+                         "write_bytes": int(write)}
+        total += fetch + write
+    out = {"workload": w, "round": tag, "hbm_bytes_per_build": int(total), "kernels": kernels,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
+                     "(tools/gpu_prof.sh); FETCH_SIZE x2 (gfx950); KiB -> bytes; median per "
+                     "dispatch of each build kernel's largest grid, summed over the build"}
+    path = os.path.join(ROOT, "profiles", f"pmc_{w}.json")
+    json.dump(out, open(path, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
