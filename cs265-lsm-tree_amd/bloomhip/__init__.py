@@ -40,9 +40,10 @@ BUILD_PARTITION = 3
 PROBE_AUTO = 0
 PROBE_GATHER = 1
 PROBE_PARTITION = 2
+PROBE_LDS = 3
 STRATEGY_NAMES = {BUILD_AUTO: "auto", BUILD_ATOMIC: "atomic", BUILD_LDS: "lds",
                   BUILD_PARTITION: "partition"}
-PROF_SLOTS = 8
+PROF_SLOTS = 9
 
 # Every symbol include/bloomhip.h and include/bloomhip_workload.h declare.
 EXPORTED_SYMBOLS = (

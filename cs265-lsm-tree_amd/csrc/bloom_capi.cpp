@@ -68,10 +68,11 @@ enum ProfSlot {
     SLOT_PROBE = 5,
     SLOT_PROBE_PART = 6,
     SLOT_COPY = 7,
+    SLOT_PROBE_LDS = 8,
 };
 const char *kSlotNames[BLOOMHIP_PROF_SLOTS] = {
-    "clear(memset)",          "k_build_atomic", "k_build_lds",      "k_part_bin",
-    "k_part_apply",           "k_probe",        "probe_partitioned", "copy",
+    "clear(memset)", "k_build_atomic", "k_build_lds",       "k_part_bin", "k_part_apply",
+    "k_probe",       "probe_partitioned", "copy",           "k_probe_lds",
 };
 
 struct PendingTiming {
@@ -282,15 +283,27 @@ int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
     return BLOOMHIP_OK;
 }
 
-bool probe_partitioned(const bloomhip_filter *f, int owner_strategy, size_t n) {
-    if (!partition_able(f)) return false;
+bool lds_probe_able(const bloomhip_filter *f) {
+    return f->mp.fast && f->nwords64 * 8 <= kLdsBitmapBytes;
+}
+
+// How filter f is probed in a batch of n keys: its own strategy, else the
+// batch owner's, else AUTO.  A strategy that cannot apply to f (LDS for a
+// filter larger than LDS, PARTITION for m >= 2^32) falls back to gathers.
+int probe_kind(const bloomhip_filter *f, int owner_strategy, size_t n) {
     const int st = f->probe_strategy != BLOOMHIP_PROBE_AUTO ? f->probe_strategy : owner_strategy;
-    if (st == BLOOMHIP_PROBE_PARTITION) return true;
-    if (st == BLOOMHIP_PROBE_GATHER) return false;
-    // AUTO: gathers while the filter stays in each XCD's L2; beyond that the
-    // MALL's random-line rate caps gathers and the partitioned probe wins
-    // (DESIGN.md §5).
-    return (f->m + 7) / 8 > kProbeGatherMaxBytes && n >= kProbePartitionMinKeys;
+    if (st == BLOOMHIP_PROBE_PARTITION)
+        return partition_able(f) ? BLOOMHIP_PROBE_PARTITION : BLOOMHIP_PROBE_GATHER;
+    if (st == BLOOMHIP_PROBE_LDS)
+        return lds_probe_able(f) ? BLOOMHIP_PROBE_LDS : BLOOMHIP_PROBE_GATHER;
+    if (st == BLOOMHIP_PROBE_GATHER) return BLOOMHIP_PROBE_GATHER;
+    // AUTO (tools/probe_sweep.py): LDS-sized filters from LDS
+    // once the batch amortises the staging; gathers while the filter mostly
+    // hits in L2 / MALL; beyond that the partitioned probe.
+    if (lds_probe_able(f) && n >= kProbeLdsMinKeys) return BLOOMHIP_PROBE_LDS;
+    if (partition_able(f) && (f->m + 7) / 8 > kProbeGatherMaxBytes && n >= kProbePartitionMinKeys)
+        return BLOOMHIP_PROBE_PARTITION;
+    return BLOOMHIP_PROBE_GATHER;
 }
 
 // Issues a clear() that was deferred (see bloomhip_clear) on stream s.
@@ -538,12 +551,21 @@ int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const voi
         HIP_TRY(grow(&f0->d_out_stage, &f0->out_stage_bytes, out_bytes));
         dout = reinterpret_cast<uint64_t *>(f0->d_out_stage);
     }
-    // Large filters: partitioned probe, one filter at a time; the rest:
-    // gathers, up to kMaxProbeFilters per launch.
+    // Small filters: LDS probe, large ones: partitioned probe, one filter at
+    // a time; the rest: gathers, up to kMaxProbeFilters per launch.
     std::vector<int> gather_idx;
     for (int j = 0; j < nf; j++) {
-        if (!probe_partitioned(filters[j], f0->probe_strategy, n)) {
+        const int kind = probe_kind(filters[j], f0->probe_strategy, n);
+        if (kind == BLOOMHIP_PROBE_GATHER) {
             gather_idx.push_back(j);
+            continue;
+        }
+        if (kind == BLOOMHIP_PROBE_LDS) {
+            hipError_t e = timed(f0, SLOT_PROBE_LDS, s, [&] {
+                return launch_probe_lds(ks, filters[j]->mp, filters[j]->d_words,
+                                        dout + (size_t)j * nw, nw, s);
+            });
+            if (e != hipSuccess) return fail_hip(e, "k_probe_lds launch");
             continue;
         }
         Workspace *w = workspace_for(f0->device, s);
@@ -654,7 +676,7 @@ int bloomhip_set_strategy(bloomhip_filter *f, int strategy) {
 
 int bloomhip_set_probe_strategy(bloomhip_filter *f, int strategy) {
     g_last_error.clear();
-    if (!f || strategy < BLOOMHIP_PROBE_AUTO || strategy > BLOOMHIP_PROBE_PARTITION)
+    if (!f || strategy < BLOOMHIP_PROBE_AUTO || strategy > BLOOMHIP_PROBE_LDS)
         return BLOOMHIP_EINVAL;
     std::lock_guard<std::mutex> lk(f->mu);
     f->probe_strategy = strategy;

@@ -57,6 +57,9 @@ constexpr size_t kPartMaxBins = 4096;  // sub-segments sorted by pass 1
 // partition 247 us for the 5 MiB level-3 filter, 531 vs 259 us for the
 // 20 MiB level 4 (gathers then miss the 4 MiB per-XCD L2 on most probes).
 constexpr size_t kProbeGatherMaxBytes = 8u << 20;
+// Filters of at most kLdsBitmapBytes are probed from LDS (k_probe_lds) once
+// the batch has this many keys (each workgroup stages the whole filter).
+constexpr size_t kProbeLdsMinKeys = 1u << 16;
 constexpr size_t kProbePartitionMinKeys = 1u << 18;
 
 struct PartitionWorkspace {
@@ -87,6 +90,10 @@ hipError_t launch_part_bin(const KeySpan &keys, const ModParams &mp, const Parti
 // merge_existing: OR into the current bitmap instead of overwriting segments.
 hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const PartitionWorkspace &ws,
                              int merge_existing, hipStream_t stream);
+// Probe of one filter with m/8 <= kLdsBitmapBytes staged in LDS; out[w]
+// packs keys 64w .. 64w+63.
+hipError_t launch_probe_lds(const KeySpan &keys, const ModParams &mp, const uint32_t *words,
+                            uint64_t *out, size_t nw_out, hipStream_t stream);
 hipError_t launch_probe(const KeySpan &keys, const ProbeTable &t, uint64_t *out, size_t nwords_out,
                         hipStream_t stream);
 // Partitioned probe of one filter (fast mod, nbins <= kPartMaxBins): bin the

@@ -464,14 +464,17 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
         if constexpr (PROBE && ABLATE == 0) {
             // the 4 result bytes go out as one dword when all 4 entries are
             // this segment's (inside a run), else byte by byte
+            // LDS reads unconditional (word 0 for other segments' entries),
+            // so the four issue back to back under one wait
             const uint32_t o[4] = {v.x - base, v.y - base, v.z - base, v.w - base};
-            uint32_t bits = 0, mask = 0;
+            uint32_t w[4], bits = 0, mask = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) w[k] = seg[o[k] < lim ? o[k] >> 5 : 0u];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                if (o[k] < lim) {
-                    mask |= 1u << k;
-                    bits |= ((seg[o[k] >> 5] >> (o[k] & 31)) & 1u) << (8 * k);
-                }
+                const uint32_t ok = o[k] < lim ? 1u : 0u;
+                mask |= ok << k;
+                bits |= (((w[k] >> (o[k] & 31)) & ok) << (8 * k));
             }
             uint8_t *p = res + (size_t)t * kPartTilePos + e;
             if (mask == 0xFu) {
@@ -591,6 +594,45 @@ __global__ void __launch_bounds__(kBlock) k_probe(KeySpan ks, ProbeTable t,
                 if (lane == 0 && g + q < t.nf) out[(size_t)(g + q) * nw_out + w] = ballot;
             }
         }
+    }
+}
+
+// LDS probe (k_probe_lds): filters of at most kLdsBitmapBytes are staged
+// whole into each workgroup's LDS (one 1024-thread workgroup per CU), then
+// every key of the grid-stride loop tests its three bits there: random LDS
+// reads run ~10x the L2 gather rate.  All three bits are
+// read (branch-free; an LDS read costs less than the divergence), the AND is
+// the reference's && result.
+constexpr int kProbeLdsBlock = 1024;
+
+template <int LAYOUT>
+__global__ void __launch_bounds__(kProbeLdsBlock) k_probe_lds(KeySpan ks, const uint32_t *words,
+                                                             ModParams mp, uint32_t nw32,
+                                                             uint64_t *__restrict__ out,
+                                                             size_t nw_out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t filt[];
+    const uint2 *src = reinterpret_cast<const uint2 *>(words);  // nw32 is even
+    for (uint32_t q = threadIdx.x; q < nw32 / 2; q += kProbeLdsBlock)
+        reinterpret_cast<uint2 *>(filt)[q] = src[q];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    constexpr int kWaves = kProbeLdsBlock / 64;
+    for (size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6); w < nw_out;
+         w += (size_t)gridDim.x * kWaves) {
+        const size_t i = w * 64 + lane;
+        const bool valid = i < ks.n;
+        int32_t k = 0;
+        if (valid) {
+            if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
+            else k = load_key(ks, i);
+        }
+        const uint32_t p1 = mod_fast(raw_hash1(k), mp);
+        const uint32_t p2 = mod_fast(raw_hash2(k), mp);
+        const uint32_t p3 = mod_fast(raw_hash3(k), mp);
+        const uint32_t hit = (filt[p1 >> 5] >> (p1 & 31)) & (filt[p2 >> 5] >> (p2 & 31)) &
+                             (filt[p3 >> 5] >> (p3 & 31)) & 1u;
+        const uint64_t ballot = __ballot(valid && hit);
+        if (lane == 0) out[w] = ballot;
     }
 }
 
@@ -816,6 +858,34 @@ hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, cons
     e = launch_apply<true>(ws, mp.m, w, nw32, 0, res, stream);
     if (e != hipSuccess) return e;
     k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_probe_lds(const KeySpan &ks, const ModParams &mp, const uint32_t *words,
+                            uint64_t *out, size_t nw_out, hipStream_t stream) {
+    if (nw_out == 0) return hipSuccess;
+    const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
+    if (!mp.fast || nw32 * 4 > kLdsBitmapBytes) return hipErrorInvalidValue;
+    static const bool attr_set = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_probe_lds<KEYS_PACKED>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBitmapBytes);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_probe_lds<KEYS_STRIDED>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBitmapBytes);
+        return true;
+    }();
+    (void)attr_set;
+    // each workgroup stages the filter once: give it >= 64 waves of keys;
+    // two workgroups per CU when two copies fit the CU's LDS
+    const size_t lds = (size_t)nw32 * 4;
+    const unsigned per_cu = lds * 2 <= kLdsBitmapBytes ? 2u : 1u;
+    const unsigned grid =
+        grid_for(nw_out, 64 * (kProbeLdsBlock / 64), per_cu * (unsigned)device_cu_count());
+    if (ks.layout == KEYS_PACKED)
+        k_probe_lds<KEYS_PACKED><<<grid, kProbeLdsBlock, lds, stream>>>(ks, words, mp,
+                                                                       (uint32_t)nw32, out, nw_out);
+    else
+        k_probe_lds<KEYS_STRIDED><<<grid, kProbeLdsBlock, lds, stream>>>(
+            ks, words, mp, (uint32_t)nw32, out, nw_out);
     return hipGetLastError();
 }
 

@@ -134,6 +134,9 @@ extern "C" int ubench_part_bin(int ablate, const void *keys, size_t n, uint64_t 
         case 4: k_part_bin<KEYS_PACKED, 0, false, true><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
         case 5: k_part_bin<KEYS_PACKED, 0, false, false><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, rows, nbins, nsub, ssh, grp, ntiles, nullptr); break;
         case 6: if (launch_runs_transpose(ws, s) != hipSuccess) return -5; break;
+        case 7:  // pass 1 (columns) with one workgroup per CU, leaving LDS for a concurrent pass 2
+            k_part_bin<KEYS_PACKED, 0, false, true><<<(unsigned)device_cu_count(), kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr);
+            break;
         default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;

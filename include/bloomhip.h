@@ -62,9 +62,10 @@ extern "C" {
 #define BLOOMHIP_BUILD_PARTITION 3 /* hash+bin pass, then LDS segment pass */
 
 /* Probe strategies for bloomhip_test_batch (bloomhip_set_probe_strategy). */
-#define BLOOMHIP_PROBE_AUTO 0      /* gather for L2-sized filters, else partition */
+#define BLOOMHIP_PROBE_AUTO 0      /* LDS for LDS-sized filters, gather up to 8 MiB, else partition */
 #define BLOOMHIP_PROBE_GATHER 1    /* per-key gathers of the 3 bits */
 #define BLOOMHIP_PROBE_PARTITION 2 /* bin positions by segment, test in LDS */
+#define BLOOMHIP_PROBE_LDS 3       /* whole filter staged in each workgroup's LDS (m/8 <= 160 KiB) */
 
 typedef struct bloomhip_filter bloomhip_filter;
 
@@ -140,7 +141,7 @@ int bloomhip_resolve_strategy(const bloomhip_filter *f, size_t n, int *strategy_
  * is bracketed by HIP events on its stream; bloomhip_profile_read returns,
  * for kernel slot `slot` (0..BLOOMHIP_PROF_SLOTS-1), its name, launch count
  * and summed device milliseconds (it synchronises the stream). */
-#define BLOOMHIP_PROF_SLOTS 8
+#define BLOOMHIP_PROF_SLOTS 9
 int bloomhip_profile_enable(bloomhip_filter *f, int enable);
 int bloomhip_profile_read(bloomhip_filter *f, int slot, const char **name_out,
                           uint64_t *launches_out, double *ms_out);

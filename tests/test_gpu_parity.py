@@ -195,16 +195,17 @@ def test_deferred_clear_then_build_and_probe(coracle, strategy):
 
 
 # ---------------------------------------------------------------- probe ----
-PROBES = [bh.PROBE_GATHER, bh.PROBE_PARTITION]
+PROBES = [bh.PROBE_GATHER, bh.PROBE_PARTITION, bh.PROBE_LDS]
+PROBE_IDS = ["gather", "partition", "lds"]
 
 
 @pytest.mark.parametrize("m", [1, 64, 65, 1000, 655_360, 1_000_003, 167_772_160, 671_088_640,
                                2**32 - 1, 2**32 + 15])
-@pytest.mark.parametrize("probe", PROBES, ids=["gather", "partition"])
+@pytest.mark.parametrize("probe", PROBES, ids=PROBE_IDS)
 def test_probe_matches_oracle(coracle, m, probe):
     keys = rand_keys(100_000 if m < 2**32 else 20_000, 21)
     f = bh.BloomFilter(m)
-    f.set_probe_strategy(probe)   # partition falls back to gathers where it cannot apply
+    f.set_probe_strategy(probe)   # partition / lds fall back to gathers where they cannot apply
     f.set_batch(keys)
     probe = np.concatenate([keys[:30_000], rand_keys(70_001, 22)])
     got = bh.test_batch([f], probe)[0]
@@ -214,14 +215,15 @@ def test_probe_matches_oracle(coracle, m, probe):
 
 def test_probe_many_filters_chunks_past_16(coracle):
     """20 filters, mixed strategies: gathered ones go out in launches of <= 16
-    consecutive rows around the partitioned ones."""
+    consecutive rows around the partitioned and LDS-probed ones."""
     rng = np.random.default_rng(3)
     filters, refs = [], []
     for j in range(20):
-        m = int(rng.integers(1000, 30_000_000))
+        m = int(rng.integers(1000, 1_300_000 if j in (5, 6, 15) else 30_000_000))
         keys = rand_keys(20_000, 100 + j)
         f = bh.BloomFilter(m)
-        f.set_probe_strategy(bh.PROBE_PARTITION if j in (3, 11, 12) else bh.PROBE_GATHER)
+        f.set_probe_strategy(bh.PROBE_PARTITION if j in (3, 11, 12) else
+                             bh.PROBE_LDS if j in (5, 6, 15) else bh.PROBE_GATHER)
         f.set_batch(keys)
         filters.append(f)
         refs.append((m, coracle.build(m, keys)))
@@ -232,10 +234,10 @@ def test_probe_many_filters_chunks_past_16(coracle):
         assert (got[j] == coracle.test(w, m, probe)).all(), j
 
 
-@pytest.mark.parametrize("probe", PROBES, ids=["gather", "partition"])
+@pytest.mark.parametrize("probe", PROBES, ids=PROBE_IDS)
 def test_probe_device_buffers_and_strides(coracle, torch_cuda, probe):
     torch = torch_cuda
-    m = 2_000_003
+    m = 1_000_003 if probe == bh.PROBE_LDS else 2_000_003
     keys = rand_keys(64 * 1000 + 37, 31)
     f = bh.BloomFilter(m)
     f.set_probe_strategy(probe)
@@ -273,7 +275,7 @@ def test_c2_full_bitmap(golden):
         assert int(np.unpackbits(w.view(np.uint8)).sum()) == golden["reference"]["c2_popcount"]
 
 
-@pytest.mark.parametrize("probe", [bh.PROBE_AUTO] + PROBES, ids=["auto", "gather", "partition"])
+@pytest.mark.parametrize("probe", [bh.PROBE_AUTO] + PROBES, ids=["auto"] + PROBE_IDS)
 def test_c3_probe_five_levels(golden, probe):
     from bloomhip import workloads as W
     gets, levels = W.c3()

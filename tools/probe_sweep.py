@@ -43,7 +43,10 @@ def main():
     ref = None
     for (lvl, _, m), f in zip(levels, filters):
         row = {}
-        for name, st in (("gather", bh.PROBE_GATHER), ("partition", bh.PROBE_PARTITION)):
+        for name, st in (("gather", bh.PROBE_GATHER), ("partition", bh.PROBE_PARTITION),
+                         ("lds", bh.PROBE_LDS)):
+            if st == bh.PROBE_LDS and (m + 7) // 8 > 160 * 1024:
+                continue
             f.set_probe_strategy(st)
             ms = timed(lambda s: bh.test_batch([f], dgets, out=out[lvl:lvl + 1], stream=s))
             row[name] = round(ms * 1e3, 1)

@@ -89,6 +89,68 @@ def part_ablation(n=16_777_216, bpe=10.0):
                               "us": round(a.elapsed_time(b) / 10 * 1e3, 2)}), flush=True)
 
 
+def overlap(n=16_777_216, bpe=10.0):
+    """Does pass 1 of one half-batch overlap pass 2 of the other on two
+    streams?  Times bin(A) apply(A) bin(B) apply(B) on one stream against
+    bin(A); {bin(B) || apply(A)}; apply(B), for both pass-1 grids."""
+    sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
+    import bloomhip as bh
+    m = bh.m_bits(n, bpe)
+    half = n // 2
+    keys = torch.from_numpy(bh.gen_puts(13141, n)).cuda()
+    ka, kb = keys[:half], keys[half:]
+    ntiles = (half + 4095) // 4096
+    bufs = []
+    for _ in range(2):
+        bufs.append((torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda"),
+                     torch.empty(ntiles * 4097 * 2, dtype=torch.int32, device="cuda")))
+    words = torch.zeros((m + 63) // 64 * 2, dtype=torch.int32, device="cuda")
+    s1 = torch.cuda.current_stream()
+    s2 = torch.cuda.Stream()
+
+    def binp(variant, k, b, s):
+        rc = LIB.ubench_part_bin(variant, k.data_ptr(), k.numel(), m, b[0].data_ptr(),
+                                 b[1].data_ptr(), s.cuda_stream)
+        assert rc == 0, rc
+
+    def apply(k, b, s):
+        rc = LIB.ubench_part_apply(0, b[0].data_ptr(), b[1].data_ptr(), k.numel(), m,
+                                   words.data_ptr(), s.cuda_stream)
+        assert rc == 0, rc
+
+    def seq(variant):
+        binp(variant, ka, bufs[0], s1)
+        apply(ka, bufs[0], s1)
+        binp(variant, kb, bufs[1], s1)
+        apply(kb, bufs[1], s1)
+
+    def ovl(variant):
+        binp(variant, ka, bufs[0], s1)
+        e = torch.cuda.Event()
+        e.record(s1)
+        s2.wait_event(e)
+        apply(ka, bufs[0], s2)
+        binp(variant, kb, bufs[1], s1)
+        e2 = torch.cuda.Event()
+        e2.record(s2)
+        s1.wait_event(e2)
+        apply(kb, bufs[1], s1)
+
+    for name, fn, v in (("seq grid2x", seq, 4), ("ovl grid2x", ovl, 4), ("seq grid1x", seq, 7),
+                        ("ovl grid1x", ovl, 7)):
+        for _ in range(3):
+            fn(v)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s1)
+        for _ in range(20):
+            fn(v)
+        b.record(s1)
+        torch.cuda.synchronize()
+        print(json.dumps({"op": "half-batch pipeline", "mode": name,
+                          "us": round(a.elapsed_time(b) / 20 * 1e3, 2)}), flush=True)
+
+
 def main():
     torch.cuda.set_device(0)
     if len(sys.argv) > 1 and sys.argv[1] == "isa":
@@ -97,6 +159,8 @@ def main():
         return part_ablation()
     if len(sys.argv) > 1 and sys.argv[1] == "part_c5":
         return part_ablation(67_108_864, 10.0)
+    if len(sys.argv) > 1 and sys.argv[1] == "overlap":
+        return overlap()
     if len(sys.argv) > 1 and sys.argv[1] == "part_c4":
         return part_ablation(268_435_456, 12.0)
     grid, block = 2048, 256
