@@ -157,11 +157,20 @@ def main():
     from bloomhip import shard
     from bloomhip import workloads as W
 
+    # One process per GPU over RCCL.  BLOOMHIP_DIST_BACKEND=gloo rehearses the
+    # N > 1 path with several ranks sharing the visible GPUs (CPU collectives).
+    backend = os.environ.get("BLOOMHIP_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
+    coll_dev = "cuda" if backend == "nccl" else None
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
 
     n, bpe = WORKLOADS[args.workload]
     seed = W.SEED + rank
@@ -212,7 +221,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        elapsed = shard.max_over_ranks(elapsed, dist, device="cuda")
+        elapsed = shard.max_over_ranks(elapsed, dist, device=coll_dev)
 
     # Per-kernel device time: the same K steps again with every launch
     # bracketed by HIP events on the launch stream (kept out of the timed
@@ -227,7 +236,7 @@ def main():
     f.profile(False)
 
     if dist:
-        all_ok = shard.all_ranks_ok(verified is not False, dist, device="cuda")
+        all_ok = shard.all_ranks_ok(verified is not False, dist, device=coll_dev)
     else:
         all_ok = verified is not False
 

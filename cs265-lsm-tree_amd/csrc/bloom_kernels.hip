@@ -139,6 +139,11 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};
+
 template <int LAYOUT>
 __device__ __forceinline__ void load_tile_keys(const KeySpan &ks, size_t tile, int tid,
                                                int32_t (&k)[kPartKPT]) {
@@ -198,36 +203,40 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     int32_t kcur[kPartKPT], knext[kPartKPT];
-    size_t tile = part_tile(0, ntiles);
-    if (tile < ntiles) load_tile_keys<LAYOUT>(ks, tile, tid, kcur);
 
-    for (size_t round = 0; tile < ntiles; round++) {
+    // One tile.  FULL (every tile but a short last one) makes the key count a
+    // constant: no per-key guards, and a fixed number of vector-memory ops
+    // after the next tile's key loads, so the wait for those keys at the top
+    // of the next tile is vmcnt(#stores) instead of a drain of every store.
+    // Those loads are issued after the run-start stores for that reason.
+    auto do_tile = [&](auto full_c, size_t tile, size_t next) {
+        constexpr bool FULL = decltype(full_c)::value;
         const size_t tile0 = tile * kPartTileKeys;
-        const int tile_keys = (int)min((size_t)kPartTileKeys, ks.n - tile0);
+        const int tile_keys = FULL ? (int)kPartTileKeys : (int)min((size_t)kPartTileKeys, ks.n - tile0);
+        auto live = [&](int j) { return FULL || j * kPartBlock + tid < tile_keys; };
         for (int b = tid; b <= nsub; b += kPartBlock) s_hist[b] = 0;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
-        const size_t next = part_tile(round + 1, ntiles);
-        if (next < ntiles) load_tile_keys<LAYOUT>(ks, next, tid, knext);
 
         // 1. positions, and each one's rank inside its sub-segment (LDS
-        //    atomics).  br[] keeps (sub-segment << 16) | rank (sub < 4096,
-        //    rank < 12288).
+        //    atomics).  The ranks are not consumed before the barrier, so all
+        //    24 atomics of a thread stay in flight behind the hashing.
         uint32_t pos[kPartKPT * 3];
-        uint32_t br[kPartKPT * 3];
+        uint32_t rank[kPartKPT * 3];
 #pragma unroll
         for (int j = 0; j < kPartKPT; j++) {
-            if (j * kPartBlock + tid < tile_keys) {
+            if (live(j)) {
                 const int32_t k = kcur[j];
                 pos[3 * j + 0] = pos32(raw_hash1(k), mp);
                 pos[3 * j + 1] = pos32(raw_hash2(k), mp);
                 pos[3 * j + 2] = pos32(raw_hash3(k), mp);
                 if constexpr (ABLATE < 3) {
 #pragma unroll
-                    for (int h = 0; h < 3; h++) {
-                        const uint32_t sub = pos[3 * j + h] >> sub_shift;
-                        br[3 * j + h] = (sub << 16) | atomicAdd(&s_hist[sub], 1u);
-                    }
+                    for (int h = 0; h < 3; h++)
+                        rank[3 * j + h] = atomicAdd(&s_hist[pos[3 * j + h] >> sub_shift], 1u);
                 }
+            } else {
+#pragma unroll
+                for (int h = 0; h < 3; h++) pos[3 * j + h] = rank[3 * j + h] = 0;
             }
         }
         if constexpr (ABLATE == 3) {
@@ -235,10 +244,8 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
 #pragma unroll
             for (int j = 0; j < kPartKPT * 3; j++) acc ^= pos[j];
             if (acc == 0x9E3779B9u) pos_out[tid] = acc;
-#pragma unroll
-            for (int j = 0; j < kPartKPT; j++) kcur[j] = knext[j];
-            tile = next;
-            continue;
+            if (next < ntiles) load_tile_keys<LAYOUT>(ks, next, tid, knext);
+            return;
         }
         lds_barrier();
 
@@ -280,20 +287,23 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
             for (int b = tid; b <= nbins; b += kPartBlock)
                 row[b] = s_hist[b == nbins ? nsub : b * group];
         }
+        if (next < ntiles) load_tile_keys<LAYOUT>(ks, next, tid, knext);
 
         if constexpr (ABLATE < 2) {
-            // 3. scatter into the LDS image sorted by segment.
+            // 3. scatter into the LDS image sorted by sub-segment: all 24
+            //    bin-offset reads first (one wait), then the writes.
+            uint32_t slot[kPartKPT * 3];
+#pragma unroll
+            for (int q = 0; q < kPartKPT * 3; q++) slot[q] = s_hist[pos[q] >> sub_shift] + rank[q];
 #pragma unroll
             for (int j = 0; j < kPartKPT; j++) {
-                if (j * kPartBlock + tid < tile_keys) {
+                if (live(j)) {
 #pragma unroll
                     for (int h = 0; h < 3; h++) {
-                        const uint32_t b = br[3 * j + h];
-                        const uint32_t slot = s_hist[b >> 16] + (b & 0xFFFFu);
-                        s_sorted[slot] = pos[3 * j + h];  // full position
+                        s_sorted[slot[3 * j + h]] = pos[3 * j + h];  // full position
                         if constexpr (SLOTS)
                             slots[(tile * 3 + h) * kPartTileKeys + j * kPartBlock + tid] =
-                                (uint16_t)slot;
+                                (uint16_t)slot[3 * j + h];
                     }
                 }
             }
@@ -302,22 +312,47 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
 
         if constexpr (ABLATE == 0) {
             // 4. the sorted tile goes out with 16-byte stores.
-            const int npos = tile_keys * 3;
             uint32_t *dst = pos_out + tile * (size_t)kPartTilePos;
-            const int nq = npos / 4;
-            for (int q = tid; q < nq; q += kPartBlock)
-                reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(s_sorted)[q];
-            for (int e = nq * 4 + tid; e < npos; e += kPartBlock) dst[e] = s_sorted[e];
-            // the short last tile: pad with a position no segment holds, since
-            // pass 2 reads whole 16-B vectors and past run ends
-            for (int e = npos + tid; e < kPartTilePos; e += kPartBlock) dst[e] = 0xFFFFFFFFu;
+            if constexpr (FULL) {
+                // exactly kStores unconditional stores per thread
+                constexpr int kStores = kPartTilePos / 4 / kPartBlock;
+                static_assert(kStores * 4 * kPartBlock == kPartTilePos, "whole 16-B stores");
+                uint4 v[kStores];
+#pragma unroll
+                for (int r = 0; r < kStores; r++)
+                    v[r] = reinterpret_cast<const uint4 *>(s_sorted)[r * kPartBlock + tid];
+#pragma unroll
+                for (int r = 0; r < kStores; r++)
+                    reinterpret_cast<uint4 *>(dst)[r * kPartBlock + tid] = v[r];
+            } else {
+                const int npos = tile_keys * 3;
+                const int nq = npos / 4;
+                for (int q = tid; q < nq; q += kPartBlock)
+                    reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(s_sorted)[q];
+                for (int e = nq * 4 + tid; e < npos; e += kPartBlock) dst[e] = s_sorted[e];
+                // the short last tile: pad with a position no segment holds,
+                // since pass 2 reads whole 16-B vectors and past run ends
+                for (int e = npos + tid; e < kPartTilePos; e += kPartBlock) dst[e] = 0xFFFFFFFFu;
+            }
         } else if constexpr (ABLATE == 1) {
             if (s_sorted[tid] == 0xFFFFFFFFu) pos_out[tid] = 0;
         }
+    };
+
+    // Full tiles in the loop; the short last tile (index ntiles - 1, always
+    // in a block's final round) after it, so the loop sees only FULL.
+    const size_t nfull = ks.n / kPartTileKeys;
+    size_t tile = part_tile(0, ntiles);
+    if (tile < ntiles) load_tile_keys<LAYOUT>(ks, tile, tid, kcur);
+    size_t round = 0;
+    for (; tile < nfull; round++) {
+        const size_t next = part_tile(round + 1, ntiles);
+        do_tile(BoolC<true>{}, tile, next);
 #pragma unroll
         for (int j = 0; j < kPartKPT; j++) kcur[j] = knext[j];
         tile = next;
     }
+    if (tile < ntiles) do_tile(BoolC<false>{}, tile, ntiles);
 }
 
 // ---------------------------------------------------------------------------
@@ -330,7 +365,7 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
 // go through the transpose: at C4 (805 MB) the column stores cost ~2.1 ms
 // (partial-line write-backs), the transpose 0.39 ms (tools/ubench.py part*).
 // ---------------------------------------------------------------------------
-constexpr size_t kColumnTableMaxBytes = 128u << 20;
+constexpr size_t kColumnTableMaxBytes = 16u << 20;
 constexpr int kTransposeTile = 64;
 constexpr int kTransposeBlock = 256;
 
