@@ -55,7 +55,8 @@ EXPORTED_SYMBOLS = (
     "bloomhip_set_strategy", "bloomhip_set_probe_strategy", "bloomhip_resolve_strategy", "bloomhip_profile_enable",
     "bloomhip_profile_read", "bloomhip_profile_reset", "bloomhip_trim", "bloomhip_host_positions",
     "bloomhip_gen_mt19937", "bloomhip_gen_glibc_rand", "bloomhip_gen_puts",
-    "bloomhip_gen_workload",
+    "bloomhip_gen_workload", "bloomhip_set_batch_run", "bloomhip_set_run_meta",
+    "bloomhip_get_run_meta", "bloomhip_route_gets",
 )
 
 
@@ -125,6 +126,11 @@ def _lib():
             "bloomhip_gen_puts": (I, [ctypes.c_uint32, SZ, P, P]),
             "bloomhip_gen_workload": (I, [ctypes.c_uint32, SZ, SZ, ctypes.c_float, ctypes.c_float,
                                           P, P]),
+            "bloomhip_set_batch_run": (I, [P, P, SZ, SZ, I, P]),
+            "bloomhip_set_run_meta": (I, [P, P, SZ, ctypes.c_int32]),
+            "bloomhip_get_run_meta": (I, [P, P, SZ, ctypes.POINTER(SZ),
+                                          ctypes.POINTER(ctypes.c_int32)]),
+            "bloomhip_route_gets": (I, [ctypes.POINTER(P), I, P, SZ, SZ, I, P, P, P, I, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -237,6 +243,32 @@ class BloomFilter:
         _check(_lib().bloomhip_set_batch(self._h, ptr, n, stride, on_dev, _stream_ptr(stream)),
                "bloomhip_set_batch")
 
+    def set_batch_run(self, keys, n: int | None = None, stride: int = 4, stream=None) -> None:
+        """set() of a whole run written in this key order, plus its fence
+        pointers and max key (Run::put, src/run.cpp:158-174)."""
+        ptr, on_dev, keep = _ptr_of(keys)
+        if n is None:
+            nbytes = keep.nbytes if isinstance(keep, np.ndarray) else keep.numel() * keep.element_size()
+            n = nbytes // stride
+        _check(_lib().bloomhip_set_batch_run(self._h, ptr, n, stride, on_dev,
+                                             _stream_ptr(stream)), "bloomhip_set_batch_run")
+
+    def set_run_meta(self, fences, max_key: int) -> None:
+        f = np.ascontiguousarray(fences, dtype=np.int32)
+        _check(_lib().bloomhip_set_run_meta(self._h, f.ctypes.data if f.size else None, f.size,
+                                            max_key), "bloomhip_set_run_meta")
+
+    def run_meta(self):
+        """(fences int32[], max_key)."""
+        nf, mk = ctypes.c_size_t(), ctypes.c_int32()
+        _check(_lib().bloomhip_get_run_meta(self._h, None, 0, ctypes.byref(nf), None),
+               "bloomhip_get_run_meta")
+        out = np.empty(nf.value, dtype=np.int32)
+        _check(_lib().bloomhip_get_run_meta(self._h, out.ctypes.data if out.size else None,
+                                            out.size, ctypes.byref(nf), ctypes.byref(mk)),
+               "bloomhip_get_run_meta")
+        return out, mk.value
+
     def clear(self, stream=None) -> None:
         _check(_lib().bloomhip_clear(self._h, _stream_ptr(stream)), "bloomhip_clear")
 
@@ -314,6 +346,33 @@ def test_batch(filters: Sequence[BloomFilter], keys, n: int | None = None, strid
     _check(_lib().bloomhip_test_batch(arr, nf, ptr, n, stride, on_dev, optr, out_dev,
                                       _stream_ptr(stream)), "bloomhip_test_batch")
     return out
+
+
+def route_gets(runs: Sequence[BloomFilter], keys, n: int | None = None, stride: int = 4,
+               cand=None, first=None, page=None, stream=None):
+    """Batched GET routing (bloomhip_route_gets): runs newest first.  Returns
+    (cand [nruns, ceil(n/64)] uint64 packed, first int32[n], page int32[n]);
+    pass device tensors for all three to keep the outputs on the device."""
+    ptr, on_dev, keep = _ptr_of(keys)
+    if n is None:
+        nbytes = keep.nbytes if isinstance(keep, np.ndarray) else keep.numel() * keep.element_size()
+        n = nbytes // stride
+    nr = len(runs)
+    nw = (n + 63) // 64
+    if cand is None and first is None and page is None:
+        cand = np.zeros((nr, nw), dtype=np.uint64)
+        first = np.empty(n, dtype=np.int32)
+        page = np.empty(n, dtype=np.int32)
+    outs = [_ptr_of(x) if x is not None else (None, None, None) for x in (cand, first, page)]
+    devs = {o[1] for o in outs if o[0] is not None}
+    if len(devs) > 1:
+        raise ValueError("route_gets outputs must be all host or all device buffers")
+    out_dev = devs.pop() if devs else 0
+    arr = (ctypes.c_void_p * nr)(*[r.handle.value for r in runs])
+    _check(_lib().bloomhip_route_gets(arr, nr, ptr, n, stride, on_dev, outs[0][0], outs[1][0],
+                                      outs[2][0], out_dev, _stream_ptr(stream)),
+           "bloomhip_route_gets")
+    return cand, first, page
 
 
 # --- workload streams (generator/generator.c restatement) --------------------

@@ -78,6 +78,15 @@ def c3(seed: int = SEED):
     return gets, levels
 
 
+def c3_runs(seed: int = SEED):
+    """(gets, [(level, run_keys, m)]) with each level's run as the reference
+    writes it: its distinct keys in ascending order (a flush sorts the buffer,
+    src/lsm_tree.cpp:124-129; a merge emits sorted, deduplicated output,
+    src/merge.cpp:6-39).  Same filters as c3(): set() is idempotent."""
+    gets, levels = c3(seed)
+    return gets, [(lvl, np.unique(keys), m) for lvl, keys, m in levels]
+
+
 def c4(seed: int = SEED, n: int = C4_N):
     return gen_puts(seed, n), m_bits(n, C4_BPE)
 

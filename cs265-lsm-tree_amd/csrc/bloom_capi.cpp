@@ -100,6 +100,14 @@ struct bloomhip_filter {
     void *d_out_stage = nullptr;
     size_t out_stage_bytes = 0;
 
+    // run metadata (§8f rows 1, 4): d_meta[0] = max key, d_meta[1..nfences]
+    // = fence pointers; set by bloomhip_set_batch_run / bloomhip_set_run_meta
+    int32_t *d_meta = nullptr;
+    size_t meta_bytes = 0;
+    uint32_t nfences = 0;
+    void *d_route_stage = nullptr;  // first/page staging for host outputs
+    size_t route_stage_bytes = 0;
+
     bool prof = false;
     uint64_t prof_launches[BLOOMHIP_PROF_SLOTS] = {};
     double prof_ms[BLOOMHIP_PROF_SLOTS] = {};
@@ -419,6 +427,8 @@ int bloomhip_destroy(bloomhip_filter *f) {
     if (f->d_words) (void)hipFree(f->d_words);
     if (f->d_stage) (void)hipFree(f->d_stage);
     if (f->d_out_stage) (void)hipFree(f->d_out_stage);
+    if (f->d_meta) (void)hipFree(f->d_meta);
+    if (f->d_route_stage) (void)hipFree(f->d_route_stage);
     (void)hipStreamDestroy(f->stream);
     delete f;
     return BLOOMHIP_OK;
@@ -481,18 +491,13 @@ int bloomhip_clear(bloomhip_filter *f, void *stream) {
     return BLOOMHIP_OK;
 }
 
-int bloomhip_set_batch(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
-                       int keys_on_device, void *stream) {
-    if (!f) return BLOOMHIP_EINVAL;
-    if (n == 0) return BLOOMHIP_OK;
-    DeviceGuard g(f->device);
-    std::lock_guard<std::mutex> lk(f->mu);
-    hipStream_t s = pick_stream(f, stream);
-    KeySpan ks{};
-    int rc = device_keys(f, keys, n, stride_bytes, keys_on_device, s, &ks);
-    if (rc) return rc;
+namespace {
+
+// The build of keys ks into f on stream s (f->mu held).
+int build_locked(bloomhip_filter *f, const KeySpan &ks, size_t n, hipStream_t s) {
     const int strategy = resolve_strategy(f, n);
     if (!strategy_supported(f, strategy)) return BLOOMHIP_EINVAL;
+    int rc;
     if (strategy == BLOOMHIP_BUILD_PARTITION && f->pending_clear) {
         f->pending_clear = false;  // pass 2 writes every word with merge = 0
     } else {
@@ -515,42 +520,108 @@ int bloomhip_set_batch(bloomhip_filter *f, const void *keys, size_t n, size_t st
     }
     if (e != hipSuccess) return fail_hip(e, "build kernel launch");
     f->known_zero = false;
+    return BLOOMHIP_OK;
+}
+
+// Room for a run's metadata: max key + ceil(n / kFenceStride) fences.
+int meta_reserve(bloomhip_filter *f, size_t nfences) {
+    return grow(reinterpret_cast<void **>(&f->d_meta), &f->meta_bytes, (nfences + 1) * 4) ==
+                   hipSuccess
+               ? BLOOMHIP_OK
+               : fail_hip(hipErrorOutOfMemory, "run metadata allocation");
+}
+
+}  // namespace
+
+int bloomhip_set_batch(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
+                       int keys_on_device, void *stream) {
+    if (!f) return BLOOMHIP_EINVAL;
+    if (n == 0) return BLOOMHIP_OK;
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    hipStream_t s = pick_stream(f, stream);
+    KeySpan ks{};
+    int rc = device_keys(f, keys, n, stride_bytes, keys_on_device, s, &ks);
+    if (rc) return rc;
+    rc = build_locked(f, ks, n, s);
+    if (rc) return rc;
     if (!keys_on_device) HIP_TRY(hipStreamSynchronize(s));
     return BLOOMHIP_OK;
 }
 
-int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const void *keys, size_t n,
-                        size_t stride_bytes, int keys_on_device, uint64_t *out_packed,
-                        int out_on_device, void *stream) {
-    if (!filters || nf <= 0 || !out_packed) return BLOOMHIP_EINVAL;
-    for (int j = 0; j < nf; j++)
-        if (!filters[j] || filters[j]->device != filters[0]->device) return BLOOMHIP_EINVAL;
-    if (n == 0) return BLOOMHIP_OK;
-    // Staging and profiling state live on the first handle.
-    bloomhip_filter *f0 = const_cast<bloomhip_filter *>(filters[0]);
-    DeviceGuard g(f0->device);
-    std::lock_guard<std::mutex> lk(f0->mu);
-    hipStream_t s = pick_stream(f0, stream);
+int bloomhip_set_batch_run(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
+                           int keys_on_device, void *stream) {
+    g_last_error.clear();
+    if (!f) return BLOOMHIP_EINVAL;
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    hipStream_t s = pick_stream(f, stream);
     KeySpan ks{};
-    int rc = device_keys(f0, keys, n, stride_bytes, keys_on_device, s, &ks);
+    int rc = device_keys(f, keys, n, stride_bytes, keys_on_device, s, &ks);
     if (rc) return rc;
-    for (int j = 0; j < nf; j++) {
-        bloomhip_filter *fj = const_cast<bloomhip_filter *>(filters[j]);
-        if (fj != f0) {
-            std::lock_guard<std::mutex> lj(fj->mu);
-            rc = materialize_clear(fj, s);
-        } else {
-            rc = materialize_clear(fj, s);
-        }
+    if (n) {
+        rc = build_locked(f, ks, n, s);
         if (rc) return rc;
     }
-    const size_t nw = (n + 63) / 64;
-    const size_t out_bytes = (size_t)nf * nw * 8;
-    uint64_t *dout = out_packed;
-    if (!out_on_device) {
-        HIP_TRY(grow(&f0->d_out_stage, &f0->out_stage_bytes, out_bytes));
-        dout = reinterpret_cast<uint64_t *>(f0->d_out_stage);
+    const size_t nf = (n + kFenceStride - 1) / kFenceStride;
+    if (nf > 0xFFFFFFFFull) return BLOOMHIP_ERANGE;
+    rc = meta_reserve(f, nf);
+    if (rc) return rc;
+    hipError_t e = launch_run_meta(ks, f->d_meta, s);
+    if (e != hipSuccess) return fail_hip(e, "k_run_meta launch");
+    f->nfences = (uint32_t)nf;
+    if (!keys_on_device) HIP_TRY(hipStreamSynchronize(s));
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_set_run_meta(bloomhip_filter *f, const int32_t *fences, size_t nfences,
+                          int32_t max_key) {
+    g_last_error.clear();
+    if (!f || (nfences && !fences) || nfences > 0xFFFFFFFFull) return BLOOMHIP_EINVAL;
+    for (size_t i = 1; i < nfences; i++)
+        if (fences[i] < fences[i - 1]) return BLOOMHIP_EINVAL;  // a run is written sorted
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    int rc = meta_reserve(f, nfences);
+    if (rc) return rc;
+    std::vector<int32_t> h(nfences + 1);
+    h[0] = max_key;
+    for (size_t i = 0; i < nfences; i++) h[1 + i] = fences[i];
+    HIP_TRY(hipMemcpy(f->d_meta, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    f->nfences = (uint32_t)nfences;
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_get_run_meta(const bloomhip_filter *f, int32_t *fences, size_t cap,
+                          size_t *nfences_out, int32_t *max_key_out) {
+    g_last_error.clear();
+    if (!f || !nfences_out) return BLOOMHIP_EINVAL;
+    bloomhip_filter *fm = const_cast<bloomhip_filter *>(f);
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(fm->mu);
+    *nfences_out = f->nfences;
+    if (!f->d_meta) {
+        if (max_key_out) *max_key_out = INT32_MIN;
+        return BLOOMHIP_OK;
     }
+    if (fences && cap < f->nfences) return BLOOMHIP_ERANGE;
+    std::vector<int32_t> h(f->nfences + 1);
+    HIP_TRY(hipDeviceSynchronize());  // the metadata may come from any stream
+    HIP_TRY(hipMemcpy(h.data(), f->d_meta, h.size() * 4, hipMemcpyDeviceToHost));
+    if (max_key_out) *max_key_out = h[0];
+    if (fences)
+        for (size_t i = 0; i < f->nfences; i++) fences[i] = h[1 + i];
+    return BLOOMHIP_OK;
+}
+
+namespace {
+
+// is_set rows of every filter for keys ks into dout (nf x ceil(n/64)), on s
+// (f0->mu held, clears materialised).
+int probe_rows(bloomhip_filter *f0, const bloomhip_filter *const *filters, int nf,
+               const KeySpan &ks, size_t n, uint64_t *dout, hipStream_t s) {
+    const size_t nw = (n + 63) / 64;
+    int rc = BLOOMHIP_OK;
     // Small filters: LDS probe, large ones: partitioned probe, one filter at
     // a time; the rest: gathers, up to kMaxProbeFilters per launch.
     std::vector<int> gather_idx;
@@ -600,11 +671,126 @@ int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const voi
         if (e != hipSuccess) return fail_hip(e, "k_probe launch");
         j0 = j1;
     }
+    return BLOOMHIP_OK;
+}
+
+// Deferred clears of every filter, issued on s (f0->mu held).
+int materialize_all(bloomhip_filter *f0, const bloomhip_filter *const *filters, int nf,
+                    hipStream_t s) {
+    for (int j = 0; j < nf; j++) {
+        bloomhip_filter *fj = const_cast<bloomhip_filter *>(filters[j]);
+        int rc;
+        if (fj != f0) {
+            std::lock_guard<std::mutex> lj(fj->mu);
+            rc = materialize_clear(fj, s);
+        } else {
+            rc = materialize_clear(fj, s);
+        }
+        if (rc) return rc;
+    }
+    return BLOOMHIP_OK;
+}
+
+}  // namespace
+
+int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const void *keys, size_t n,
+                        size_t stride_bytes, int keys_on_device, uint64_t *out_packed,
+                        int out_on_device, void *stream) {
+    if (!filters || nf <= 0 || !out_packed) return BLOOMHIP_EINVAL;
+    for (int j = 0; j < nf; j++)
+        if (!filters[j] || filters[j]->device != filters[0]->device) return BLOOMHIP_EINVAL;
+    if (n == 0) return BLOOMHIP_OK;
+    // Staging and profiling state live on the first handle.
+    bloomhip_filter *f0 = const_cast<bloomhip_filter *>(filters[0]);
+    DeviceGuard g(f0->device);
+    std::lock_guard<std::mutex> lk(f0->mu);
+    hipStream_t s = pick_stream(f0, stream);
+    KeySpan ks{};
+    int rc = device_keys(f0, keys, n, stride_bytes, keys_on_device, s, &ks);
+    if (rc) return rc;
+    rc = materialize_all(f0, filters, nf, s);
+    if (rc) return rc;
+    const size_t nw = (n + 63) / 64;
+    const size_t out_bytes = (size_t)nf * nw * 8;
+    uint64_t *dout = out_packed;
+    if (!out_on_device) {
+        HIP_TRY(grow(&f0->d_out_stage, &f0->out_stage_bytes, out_bytes));
+        dout = reinterpret_cast<uint64_t *>(f0->d_out_stage);
+    }
+    rc = probe_rows(f0, filters, nf, ks, n, dout, s);
+    if (rc) return rc;
     if (!out_on_device) {
         hipError_t e = timed(f0, SLOT_COPY, s, [&] {
             return hipMemcpyAsync(out_packed, dout, out_bytes, hipMemcpyDeviceToHost, s);
         });
         if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(results D2H)");
+    }
+    if (!keys_on_device || !out_on_device) HIP_TRY(hipStreamSynchronize(s));
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const void *keys, size_t n,
+                        size_t stride_bytes, int keys_on_device, uint64_t *cand_packed,
+                        int32_t *first_run, int32_t *page, int out_on_device, void *stream) {
+    g_last_error.clear();
+    if (!runs || nruns <= 0 || nruns > kMaxRouteRuns) return BLOOMHIP_EINVAL;
+    for (int j = 0; j < nruns; j++)
+        if (!runs[j] || runs[j]->device != runs[0]->device) return BLOOMHIP_EINVAL;
+    if (n == 0) return BLOOMHIP_OK;
+    bloomhip_filter *f0 = const_cast<bloomhip_filter *>(runs[0]);
+    DeviceGuard g(f0->device);
+    std::lock_guard<std::mutex> lk(f0->mu);
+    hipStream_t s = pick_stream(f0, stream);
+    KeySpan ks{};
+    int rc = device_keys(f0, keys, n, stride_bytes, keys_on_device, s, &ks);
+    if (rc) return rc;
+    rc = materialize_all(f0, runs, nruns, s);
+    if (rc) return rc;
+    RouteTable t{};
+    t.nruns = nruns;
+    uint32_t off = 0;
+    for (int j = 0; j < nruns; j++) {
+        bloomhip_filter *fj = const_cast<bloomhip_filter *>(runs[j]);
+        if (!fj->d_meta) {  // no metadata: never a candidate
+            if (fj != f0) {
+                std::lock_guard<std::mutex> lj(fj->mu);
+                rc = meta_reserve(fj, 0);
+            } else {
+                rc = meta_reserve(fj, 0);
+            }
+            if (rc) return rc;
+            fj->nfences = 0;
+        }
+        t.meta[j] = fj->d_meta;
+        t.nfences[j] = fj->nfences;
+        t.fence_off[j] = off;
+        off += fj->nfences;
+    }
+    t.total_fences = off;
+    const size_t nw = (n + 63) / 64;
+    const size_t cand_bytes = (size_t)nruns * nw * 8;
+    uint64_t *dcand = out_on_device ? cand_packed : nullptr;
+    if (!dcand) {
+        HIP_TRY(grow(&f0->d_out_stage, &f0->out_stage_bytes, cand_bytes));
+        dcand = reinterpret_cast<uint64_t *>(f0->d_out_stage);
+    }
+    int32_t *dfirst = out_on_device ? first_run : nullptr;
+    int32_t *dpage = out_on_device ? page : nullptr;
+    if (!out_on_device && (first_run || page)) {
+        HIP_TRY(grow(&f0->d_route_stage, &f0->route_stage_bytes, n * 8));
+        dfirst = first_run ? reinterpret_cast<int32_t *>(f0->d_route_stage) : nullptr;
+        dpage = page ? reinterpret_cast<int32_t *>(f0->d_route_stage) + n : nullptr;
+    }
+    rc = probe_rows(f0, runs, nruns, ks, n, dcand, s);
+    if (rc) return rc;
+    hipError_t e = launch_route(ks, t, dcand, nw, dfirst, dpage, s);
+    if (e != hipSuccess) return fail_hip(e, "k_route launch");
+    if (!out_on_device) {
+        if (cand_packed)
+            HIP_TRY(hipMemcpyAsync(cand_packed, dcand, cand_bytes, hipMemcpyDeviceToHost, s));
+        if (first_run)
+            HIP_TRY(hipMemcpyAsync(first_run, dfirst, n * 4, hipMemcpyDeviceToHost, s));
+        if (page) HIP_TRY(hipMemcpyAsync(page, dpage, n * 4, hipMemcpyDeviceToHost, s));
     }
     if (!keys_on_device || !out_on_device) HIP_TRY(hipStreamSynchronize(s));
     return BLOOMHIP_OK;

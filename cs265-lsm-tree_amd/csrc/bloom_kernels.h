@@ -32,6 +32,21 @@ struct ProbeTable {
     int nf;
 };
 
+// Run metadata and GET routing (§8f rows 1, 4).
+constexpr size_t kFenceStride = 4096;  // getpagesize() entries per fence, src/run.cpp:164
+constexpr int kMaxRouteRuns = 64;
+constexpr size_t kRouteLdsFenceBytes = 48u << 10;  // fences of all runs staged in LDS up to this
+
+// Run metadata on the device: meta[0] = max key, meta[1 .. nfences] = the
+// fence pointers, ascending (a run is written sorted).
+struct RouteTable {
+    const int32_t *meta[kMaxRouteRuns];
+    uint32_t nfences[kMaxRouteRuns];
+    uint32_t fence_off[kMaxRouteRuns];  // offset of run r's fences in the LDS copy
+    uint32_t total_fences;
+    int nruns;
+};
+
 // LDS bytes a private-bitmap workgroup may use (m/8 must fit): 160 KiB per
 // CU on gfx950, one such workgroup per CU.
 constexpr size_t kLdsBitmapBytes = 160 * 1024;
@@ -96,6 +111,12 @@ hipError_t launch_probe_lds(const KeySpan &keys, const ModParams &mp, const uint
                             uint64_t *out, size_t nw_out, hipStream_t stream);
 hipError_t launch_probe(const KeySpan &keys, const ProbeTable &t, uint64_t *out, size_t nwords_out,
                         hipStream_t stream);
+// meta[0] = max key, meta[1 ..] = the ceil(n / kFenceStride) fences of a run.
+hipError_t launch_run_meta(const KeySpan &keys, int32_t *meta, hipStream_t stream);
+// Applies the range checks to the probe rows `cand` in place and writes the
+// newest candidate run and its page index per key (first/page may be null).
+hipError_t launch_route(const KeySpan &keys, const RouteTable &t, uint64_t *cand, size_t nw,
+                        int32_t *first, int32_t *page, hipStream_t stream);
 // Partitioned probe of one filter (fast mod, nbins <= kPartMaxBins): bin the
 // keys' positions by segment (recording each position's sorted slot), test
 // each segment in LDS writing one result byte per sorted entry, then AND each

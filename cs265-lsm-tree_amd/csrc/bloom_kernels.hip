@@ -700,6 +700,103 @@ __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     }
 }
 
+// ---------------------------------------------------------------------------
+// §8f rows 1 and 4: run metadata and batched GET routing.
+// k_run_meta: the fence pointers of a run written in key order (the key of
+// every entry whose index is a multiple of kFenceStride, src/run.cpp:164-166)
+// and its max key (src/run.cpp:170), built beside the filter.
+// k_route: per key, which runs Run::get would read (range check against the
+// run's first fence and max key, then the filter bit, src/run.cpp:94-96), the
+// newest such run (src/lsm_tree.cpp:141-151,195-201) and its page index
+// (upper_bound over its fences - 1, src/run.cpp:97-99).  The filter bits come
+// from the probe kernels (any strategy) in the packed rows `cand`, which are
+// rewritten in place with the range check applied.  All runs' fences are
+// staged in LDS when they fit, so the page search costs LDS reads only.
+// ---------------------------------------------------------------------------
+constexpr int kMetaBlock = 256;
+
+template <int LAYOUT>
+__global__ void __launch_bounds__(kMetaBlock) k_run_meta(KeySpan ks, int32_t *__restrict__ meta) {
+    int32_t *fences = meta + 1;
+    __shared__ int32_t s_max[kMetaBlock / 64];
+    int32_t mx = INT32_MIN;
+    for (size_t i = (size_t)blockIdx.x * kMetaBlock + threadIdx.x; i < ks.n;
+         i += (size_t)gridDim.x * kMetaBlock) {
+        int32_t k;
+        if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
+        else k = load_key(ks, i);
+        if (i % kFenceStride == 0) fences[i / kFenceStride] = k;
+        mx = max(mx, k);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kMetaBlock / 64; w++) mx = max(mx, s_max[w]);
+        atomicMax(meta, mx);  // meta[0] starts at INT32_MIN
+    }
+}
+
+constexpr int kRouteBlock = 256;
+
+template <int LAYOUT, bool LDS_FENCES>
+__global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
+                                                      uint64_t *__restrict__ cand, size_t nw,
+                                                      int32_t *__restrict__ first,
+                                                      int32_t *__restrict__ page) {
+    extern __shared__ int32_t s_fences[];
+    __shared__ int32_t s_lo[kMaxRouteRuns], s_hi[kMaxRouteRuns];
+    for (int r = threadIdx.x; r < t.nruns; r += kRouteBlock) {
+        s_hi[r] = t.meta[r][0];
+        s_lo[r] = t.nfences[r] ? t.meta[r][1] : 0;
+    }
+    if constexpr (LDS_FENCES) {
+        for (int r = 0; r < t.nruns; r++)
+            for (uint32_t i = threadIdx.x; i < t.nfences[r]; i += kRouteBlock)
+                s_fences[t.fence_off[r] + i] = t.meta[r][1 + i];
+    }
+    __syncthreads();
+    auto fence = [&](int r, uint32_t i) -> int32_t {
+        if constexpr (LDS_FENCES) return s_fences[t.fence_off[r] + i];
+        else return t.meta[r][1 + i];
+    };
+    const int lane = threadIdx.x & 63;
+    for (size_t w = ((size_t)blockIdx.x * kRouteBlock + threadIdx.x) >> 6; w < nw;
+         w += ((size_t)gridDim.x * kRouteBlock) >> 6) {
+        const size_t i = w * 64 + lane;
+        const bool valid = i < ks.n;
+        int32_t k = 0;
+        if (valid) {
+            if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
+            else k = load_key(ks, i);
+        }
+        int32_t fr = -1;
+        for (int r = 0; r < t.nruns; r++) {
+            const uint64_t bits = cand[(size_t)r * nw + w];
+            const bool c = valid && ((bits >> lane) & 1u) && t.nfences[r] > 0 &&
+                           k >= s_lo[r] && k <= s_hi[r];
+            const uint64_t b = __ballot(c);
+            if (lane == 0) cand[(size_t)r * nw + w] = b;
+            if (c && fr < 0) fr = r;
+        }
+        int32_t pg = -1;
+        if (fr >= 0) {
+            uint32_t lo = 0, hi = t.nfences[fr];  // upper_bound
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (fence(fr, mid) <= k) lo = mid + 1;
+                else hi = mid;
+            }
+            pg = (int32_t)lo - 1;
+        }
+        if (valid) {
+            if (first) first[i] = fr;
+            if (page) page[i] = pg;
+        }
+    }
+}
+
 // Persistent pass-1 grid: two 64-KiB-LDS workgroups per CU.
 inline unsigned part_bin_grid(size_t ntiles) {
     const size_t g = (size_t)device_cu_count() * 2;
@@ -921,6 +1018,35 @@ hipError_t launch_probe_lds(const KeySpan &ks, const ModParams &mp, const uint32
     else
         k_probe_lds<KEYS_STRIDED><<<grid, kProbeLdsBlock, lds, stream>>>(
             ks, words, mp, (uint32_t)nw32, out, nw_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_run_meta(const KeySpan &ks, int32_t *meta, hipStream_t stream) {
+    hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(meta), (int)INT32_MIN, 1,
+                                     stream);
+    if (e != hipSuccess || ks.n == 0) return e;
+    const unsigned grid = grid_for(ks.n, kMetaBlock * 8, 1024);
+    if (ks.layout == KEYS_PACKED)
+        k_run_meta<KEYS_PACKED><<<grid, kMetaBlock, 0, stream>>>(ks, meta);
+    else
+        k_run_meta<KEYS_STRIDED><<<grid, kMetaBlock, 0, stream>>>(ks, meta);
+    return hipGetLastError();
+}
+
+hipError_t launch_route(const KeySpan &ks, const RouteTable &t, uint64_t *cand, size_t nw,
+                        int32_t *first, int32_t *page, hipStream_t stream) {
+    if (nw == 0) return hipSuccess;
+    const unsigned grid = grid_for(nw, kRouteBlock / 64, 16384);
+    const size_t lds = (size_t)t.total_fences * 4;
+    const bool in_lds = lds <= kRouteLdsFenceBytes;
+#define ROUTE_LAUNCH(L, F) \
+    k_route<L, F><<<grid, kRouteBlock, F ? lds : 0, stream>>>(ks, t, cand, nw, first, page)
+    if (ks.layout == KEYS_PACKED) {
+        if (in_lds) ROUTE_LAUNCH(KEYS_PACKED, true); else ROUTE_LAUNCH(KEYS_PACKED, false);
+    } else {
+        if (in_lds) ROUTE_LAUNCH(KEYS_STRIDED, true); else ROUTE_LAUNCH(KEYS_STRIDED, false);
+    }
+#undef ROUTE_LAUNCH
     return hipGetLastError();
 }
 

@@ -116,6 +116,42 @@ int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const voi
                         size_t n, size_t stride_bytes, int keys_on_device,
                         uint64_t *out_packed, int out_on_device, void *stream);
 
+/* --- run metadata and batched GET routing ------
+ *
+ * bloomhip_set_batch_run: a whole run written at once (a flush,
+ * src/lsm_tree.cpp:124-129, or a compaction's output, :74-88): set() of every
+ * key as bloomhip_set_batch, plus the run's metadata that Run::put builds in
+ * the same pass (src/run.cpp:158-174): a fence pointer = the key of every
+ * entry whose index is a multiple of 4096 (getpagesize(), :164-166), and the
+ * max key (:170; the reference leaves max_key uninitialised, src/run.h:13 —
+ * here it starts at INT32_MIN).  Replaces the previous metadata. */
+int bloomhip_set_batch_run(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
+                           int keys_on_device, void *stream);
+/* Metadata of a run restored from disk (fences ascending).  Synchronous. */
+int bloomhip_set_run_meta(bloomhip_filter *f, const int32_t *fences, size_t nfences,
+                          int32_t max_key);
+/* Metadata back to the host: *nfences_out always; fences (if non-NULL,
+ * capacity cap) and *max_key_out.  Synchronous. */
+int bloomhip_get_run_meta(const bloomhip_filter *f, int32_t *fences, size_t cap,
+                          size_t *nfences_out, int32_t *max_key_out);
+
+/* Batched GET routing over nruns <= 64 runs, runs[0] the newest
+ * (LSMTree::get_run order, src/lsm_tree.cpp:141-151).  Run r is a candidate
+ * for key i when Run::get would read a page for it (src/run.cpp:94-96):
+ *     fence_r[0] <= key <= max_key_r  &&  is_set_r(key)
+ * (a run without metadata is never a candidate).  Outputs, each optional
+ * (NULL to skip):
+ *   cand_packed  nruns x ceil(n/64) u64, bit i%64 of row r word i/64;
+ *   first_run[i] the newest candidate (the run LSMTree::get settles on when
+ *                the key is there, src/lsm_tree.cpp:195-201), -1 if none;
+ *   page[i]      that run's page index, upper_bound(fences, key) - 1
+ *                (src/run.cpp:97-99), -1 if none.
+ * Reading the page and checking the key stays with the caller. */
+int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const void *keys,
+                        size_t n, size_t stride_bytes, int keys_on_device,
+                        uint64_t *cand_packed, int32_t *first_run, int32_t *page,
+                        int out_on_device, void *stream);
+
 /* Scalar compatibility entry points (one key; synchronous). */
 int bloomhip_set(bloomhip_filter *f, int32_t key);
 int bloomhip_is_set(const bloomhip_filter *f, int32_t key, int *hit_out);

@@ -146,3 +146,71 @@ uint64_t bo_popcount(const uint64_t *words, size_t nwords) {
     for (size_t i = 0; i < nwords; i++) c += (uint64_t)__builtin_popcountll(words[i]);
     return c;
 }
+
+/* ---- §8f rows 1 and 4: run metadata and batched GET routing --------------
+ *
+ * Run metadata built while a run is written (Run::put, src/run.cpp:158-174):
+ *   - a fence pointer is the key of every entry whose index is a multiple of
+ *     getpagesize() = 4096 (`if (size % getpagesize() == 0)`, :164-166);
+ *   - max_key = max over the run's keys (:170).  The reference never
+ *     initialises max_key (src/run.h:13), so its first comparison reads an
+ *     indeterminate value; the restatement (and the engine) start from
+ *     INT32_MIN, i.e. the intended maximum.
+ */
+size_t bo_run_meta(const void *keys, size_t n, size_t stride, int32_t *fences,
+                   int32_t *max_key) {
+    size_t nf = 0;
+    int32_t mx = INT32_MIN;
+    for (size_t i = 0; i < n; i++) {
+        const int32_t k = bo_key_at(keys, i, stride);
+        if (i % 4096 == 0) fences[nf++] = k;
+        if (k > mx) mx = k;
+    }
+    *max_key = mx;
+    return nf;
+}
+
+/* upper_bound(fences, fences + nf, key) - fences - 1 (src/run.cpp:97-98). */
+static long bo_page_index(const int32_t *fences, size_t nf, int32_t key) {
+    size_t lo = 0, hi = nf;
+    while (lo < hi) {
+        const size_t mid = lo + (hi - lo) / 2;
+        if (fences[mid] <= key) lo = mid + 1;
+        else hi = mid;
+    }
+    return (long)lo - 1;
+}
+
+/*
+ * Routing of n GET keys over nruns runs, runs[0] the newest
+ * (LSMTree::get_run order, src/lsm_tree.cpp:141-151).  Run r is a candidate
+ * for key k when Run::get would read a page (src/run.cpp:94-96):
+ *     fences_r[0] <= k <= max_key_r  &&  bloom_r.is_set(k)
+ * cand: nruns x ceil(n/64) packed (bit i%64 of row r word i/64);
+ * first[i]: the newest candidate run (the one LSMTree::get's workers settle
+ * on when the key is there, src/lsm_tree.cpp:195-201), -1 if none;
+ * page[i]: that run's page index (src/run.cpp:97-99), -1 if none.
+ * A run with no fence pointers (empty) is never a candidate.
+ */
+int bo_route(int nruns, const uint64_t *const *words, const uint64_t *ms,
+             const int32_t *const *fences, const size_t *nfences, const int32_t *max_keys,
+             const void *keys, size_t n, size_t stride, uint64_t *cand, int32_t *first,
+             int32_t *page) {
+    const size_t nw = (n + 63) / 64;
+    for (size_t i = 0; i < (size_t)nruns * nw; i++) cand[i] = 0;
+    for (size_t i = 0; i < n; i++) {
+        const int32_t k = bo_key_at(keys, i, stride);
+        first[i] = -1;
+        page[i] = -1;
+        for (int r = 0; r < nruns; r++) {
+            if (nfences[r] == 0 || k < fences[r][0] || k > max_keys[r]) continue;
+            if (ms[r] == 0 || !bo_is_set(words[r], ms[r], k)) continue;
+            cand[(size_t)r * nw + i / 64] |= 1ull << (i % 64);
+            if (first[i] < 0) {
+                first[i] = r;
+                page[i] = (int32_t)bo_page_index(fences[r], nfences[r], k);
+            }
+        }
+    }
+    return 0;
+}

@@ -143,6 +143,11 @@ class COracle:
         L.bo_is_set.restype = ctypes.c_int
         L.bo_popcount.argtypes = [P, ctypes.c_size_t]
         L.bo_popcount.restype = ctypes.c_uint64
+        L.bo_run_meta.argtypes = [P, ctypes.c_size_t, ctypes.c_size_t, P, P]
+        L.bo_run_meta.restype = ctypes.c_size_t
+        L.bo_route.argtypes = [ctypes.c_int, P, P, P, P, P, P, ctypes.c_size_t, ctypes.c_size_t,
+                               P, P, P]
+        L.bo_route.restype = ctypes.c_int
         self.L = L
 
     def m_bits(self, max_size: int, bpe: float) -> int:
@@ -196,3 +201,42 @@ class COracle:
     def popcount(self, words: np.ndarray) -> int:
         w = np.ascontiguousarray(words, dtype=np.uint64)
         return int(self.L.bo_popcount(w.ctypes.data, w.size))
+
+
+def _run_meta(L, keys, stride: int = 4, n: int | None = None):
+    buf = np.ascontiguousarray(keys)
+    if n is None:
+        n = buf.nbytes // stride
+    fences = np.empty(max(1, (n + 4095) // 4096), dtype=np.int32)
+    mx = ctypes.c_int32()
+    nf = L.bo_run_meta(buf.ctypes.data, n, stride, fences.ctypes.data, ctypes.byref(mx))
+    return fences[:nf].copy(), mx.value
+
+
+def _route(L, runs, keys, stride: int = 4):
+    """runs: [(words, m, fences, max_key)] newest first.  Returns
+    (cand [nruns, ceil(n/64)] uint64, first int32[n], page int32[n])."""
+    buf = np.ascontiguousarray(keys)
+    n = buf.nbytes // stride
+    nr = len(runs)
+    keep = [(np.ascontiguousarray(w, dtype=np.uint64), np.ascontiguousarray(f, dtype=np.int32))
+            for w, _, f, _ in runs]
+    W = (ctypes.c_void_p * nr)(*[k[0].ctypes.data for k in keep])
+    F = (ctypes.c_void_p * nr)(*[k[1].ctypes.data if k[1].size else None for k in keep])
+    ms = np.array([r[1] for r in runs], dtype=np.uint64)
+    nfs = np.array([k[1].size for k in keep], dtype=np.uint64)
+    mks = np.array([r[3] for r in runs], dtype=np.int32)
+    cand = np.zeros((nr, (n + 63) // 64), dtype=np.uint64)
+    first = np.empty(n, dtype=np.int32)
+    page = np.empty(n, dtype=np.int32)
+    rc = L.bo_route(nr, W, ms.ctypes.data, F, nfs.ctypes.data, mks.ctypes.data, buf.ctypes.data, n,
+                    stride, cand.ctypes.data, first.ctypes.data, page.ctypes.data)
+    if rc != 0:
+        raise ValueError(f"bo_route rc={rc}")
+    return cand, first, page
+
+
+COracle.run_meta = lambda self, keys, stride=4, n=None: _run_meta(self.L, keys, stride, n)
+COracle.run_meta.__doc__ = "(fences, max_key) of a run written in this key order (src/run.cpp:158-174)."
+COracle.route = lambda self, runs, keys, stride=4: _route(self.L, runs, keys, stride)
+COracle.route.__doc__ = _route.__doc__

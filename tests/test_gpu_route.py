@@ -1,0 +1,159 @@
+"""GPU parity of §8f rows 1 and 4: run metadata (fence pointers, max key)
+built beside the filter, and batched GET routing (range check + filter probe
++ newest candidate run + page index), against the C oracle's restatement of
+Run::put / Run::get / LSMTree::get (oracle/bloom_oracle.c bo_run_meta,
+bo_route).  Bit-exact: same fences and max key, same candidate rows, same
+first-run and page per key."""
+import numpy as np
+import pytest
+
+import bloomhip as bh
+
+pytestmark = pytest.mark.gpu
+
+
+def sorted_run(n, seed):
+    rng = np.random.default_rng(seed)
+    k = np.unique(rng.integers(-2**31, 2**31, size=n + n // 8 + 8, dtype=np.int64).astype(np.int32))
+    return k[:n] if k.size >= n else k
+
+
+@pytest.mark.parametrize("n", [0, 1, 4095, 4096, 4097, 12_289, 300_000])
+def test_run_meta_matches_oracle(coracle, n):
+    keys = sorted_run(n, n + 1)
+    f = bh.BloomFilter(bh.m_bits(max(n, 1), 10.0))
+    f.set_batch_run(keys)
+    fences, mk = f.run_meta()
+    want_f, want_mk = coracle.run_meta(keys)
+    assert np.array_equal(fences, want_f)
+    assert mk == want_mk
+    if n:
+        assert (f.words() == coracle.build(f.m, keys)).all()
+
+
+def test_run_meta_strided_unsorted_and_device(coracle):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(5)
+    keys = rng.integers(-2**31, 2**31, size=50_001, dtype=np.int64).astype(np.int32)  # unsorted
+    aos = np.zeros((keys.size, 2), dtype=np.int32)
+    aos[:, 0] = keys
+    f = bh.BloomFilter(600_000)
+    f.set_batch_run(aos.reshape(-1), n=keys.size, stride=8)
+    want = coracle.run_meta(keys)
+    got = f.run_meta()
+    assert np.array_equal(got[0], want[0]) and got[1] == want[1]
+    g = bh.BloomFilter(600_000)
+    g.set_batch_run(torch.from_numpy(keys).cuda())
+    got = g.run_meta()
+    assert np.array_equal(got[0], want[0]) and got[1] == want[1]
+
+
+def test_run_meta_upload_round_trip():
+    f = bh.BloomFilter(1000)
+    fences = np.array([-5, 3, 3, 90], dtype=np.int32)
+    f.set_run_meta(fences, 1234)
+    got = f.run_meta()
+    assert np.array_equal(got[0], fences) and got[1] == 1234
+    with pytest.raises(bh.BloomHipError):
+        f.set_run_meta(np.array([4, 1], dtype=np.int32), 9)   # fences must ascend
+
+
+def build_runs(sizes, bpe=10.0, seed=0, probe=bh.PROBE_AUTO):
+    runs, refs = [], []
+    for j, n in enumerate(sizes):
+        keys = sorted_run(n, 1000 * seed + j)
+        m = bh.m_bits(max(n, 1), bpe)
+        f = bh.BloomFilter(m)
+        f.set_probe_strategy(probe)
+        f.set_batch_run(keys)
+        runs.append(f)
+        refs.append((keys, m))
+    return runs, refs
+
+
+def oracle_runs(coracle, refs):
+    out = []
+    for keys, m in refs:
+        fences, mk = coracle.run_meta(keys)
+        out.append((coracle.build(m, keys), m, fences, mk))
+    return out
+
+
+def get_keys(refs, n, seed):
+    rng = np.random.default_rng(seed)
+    pool = np.concatenate([k for k, _ in refs])
+    hits = pool[rng.integers(0, pool.size, size=n // 2)]
+    miss = rng.integers(-2**31, 2**31, size=n - n // 2, dtype=np.int64).astype(np.int32)
+    g = np.concatenate([hits, miss])
+    rng.shuffle(g)
+    g[:4] = [np.iinfo(np.int32).min, np.iinfo(np.int32).max, refs[0][0][0], refs[0][0][-1]]
+    return g
+
+
+@pytest.mark.parametrize("probe", [bh.PROBE_AUTO, bh.PROBE_GATHER, bh.PROBE_PARTITION,
+                                   bh.PROBE_LDS], ids=["auto", "gather", "partition", "lds"])
+def test_route_matches_oracle(coracle, probe):
+    runs, refs = build_runs([20_000, 70_000, 300_000, 1_200_000, 9], seed=1, probe=probe)
+    gets = get_keys(refs, 400_001, 7)
+    cand, first, page = bh.route_gets(runs, gets)
+    wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
+    assert np.array_equal(cand, wc)
+    assert np.array_equal(first, wf)
+    assert np.array_equal(page, wp)
+    assert (first >= 0).sum() > 0 and (page[first >= 0] >= 0).all()
+
+
+def test_route_many_runs_and_missing_meta(coracle):
+    """40 runs (probe launches chunked past 16 filters); one run has no
+    metadata (never a candidate), one is empty."""
+    sizes = [int(s) for s in np.random.default_rng(2).integers(1000, 120_000, size=40)]
+    sizes[7] = 0
+    runs, refs = build_runs(sizes, seed=2)
+    nometa = bh.BloomFilter(bh.m_bits(5000, 10.0))
+    nometa.set_batch(refs[3][0][:5000])           # filter only, no set_batch_run
+    runs[12] = nometa
+    gets = get_keys(refs, 100_003, 9)
+    cand, first, page = bh.route_gets(runs, gets)
+    orefs = oracle_runs(coracle, refs)
+    orefs[12] = (coracle.build(nometa.m, refs[3][0][:5000]), nometa.m, np.zeros(0, np.int32), 0)
+    wc, wf, wp = coracle.route(orefs, gets)
+    assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
+    assert not cand[12].any() and not cand[7].any()
+
+
+def test_route_device_buffers_and_strides(coracle):
+    torch = pytest.importorskip("torch")
+    runs, refs = build_runs([50_000, 200_000], seed=3)
+    gets = get_keys(refs, 70_001, 11)
+    wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
+    n = gets.size
+    dc = torch.zeros((2, (n + 63) // 64), dtype=torch.int64, device="cuda")
+    df = torch.empty(n, dtype=torch.int32, device="cuda")
+    dp = torch.empty(n, dtype=torch.int32, device="cuda")
+    bh.route_gets(runs, torch.from_numpy(gets).cuda(), cand=dc, first=df, page=dp)
+    torch.cuda.synchronize()
+    assert np.array_equal(dc.cpu().numpy().view(np.uint64), wc)
+    assert np.array_equal(df.cpu().numpy(), wf) and np.array_equal(dp.cpu().numpy(), wp)
+    aos = np.zeros((n, 2), dtype=np.int32)
+    aos[:, 0] = gets
+    c2, f2, p2 = bh.route_gets(runs, aos.reshape(-1), n=n, stride=8)
+    assert np.array_equal(c2, wc) and np.array_equal(f2, wf) and np.array_equal(p2, wp)
+
+
+def test_route_c3_full(coracle, golden):
+    """C3 at full size: 16.8M GETs over the five level runs."""
+    from bloomhip import workloads as W
+    gets, levels = W.c3_runs()
+    runs, orefs = [], []
+    for lvl, keys, m in levels:
+        f = bh.BloomFilter(m)
+        f.set_batch_run(keys)
+        runs.append(f)
+        fences, mk = coracle.run_meta(keys)
+        orefs.append((coracle.build(m, keys), m, fences, mk))
+    cand, first, page = bh.route_gets(runs, gets)
+    wc, wf, wp = coracle.route(orefs, gets)
+    assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
+    # filter bits are the pinned C3 probe results restricted by the range check
+    probe = bh.test_batch(runs, gets)
+    assert ((cand & ~probe) == 0).all()

@@ -105,3 +105,35 @@ def test_c3_pins(coracle, golden):
         assert coracle.popcount(w) == golden["reference"]["c3_popcount"][lvl]
         hits = coracle.test(w, m, gets)
         assert int(np.unpackbits(hits.view(np.uint8)).sum()) == golden["reference"]["c3_hits"][lvl]
+
+
+def test_route_restatement_matches_python_loops(coracle):
+    """bo_run_meta / bo_route against a direct Python restatement of
+    Run::put (src/run.cpp:158-174), Run::get's checks (:94-99) and
+    LSMTree::get's newest-run pick (src/lsm_tree.cpp:141-151,195-201)."""
+    import bisect
+    from bloom_oracle import np_build, np_test_batch
+    rng = np.random.default_rng(4)
+    runs = []
+    for n in (0, 3, 5000, 9000, 20000):
+        keys = np.unique(rng.integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32))
+        m = max(1, n * 10)
+        fences = [int(k) for i, k in enumerate(keys) if i % 4096 == 0]
+        mk = int(keys.max()) if keys.size else -2**31
+        f2, mk2 = coracle.run_meta(keys)
+        assert list(f2) == fences and mk2 == mk
+        runs.append((np_build(m, keys), m, np.array(fences, np.int32), mk, keys))
+    pool = np.concatenate([r[4] for r in runs])
+    gets = np.concatenate([pool[rng.integers(0, pool.size, 3000)],
+                           rng.integers(-2**31, 2**31, 3000, dtype=np.int64).astype(np.int32)])
+    cand, first, page = coracle.route([r[:4] for r in runs], gets)
+    bits = [np_test_batch(w, m, gets) for w, m, *_ in runs]
+    for i, k in enumerate(gets.tolist()):
+        want_first, want_page = -1, -1
+        for r, (w, m, fences, mk, _) in enumerate(runs):
+            c = len(fences) > 0 and fences[0] <= k <= mk and bool(bits[r][i])
+            assert bool((int(cand[r][i // 64]) >> (i % 64)) & 1) == c
+            if c and want_first < 0:
+                want_first = r
+                want_page = bisect.bisect_right(list(fences), k) - 1
+        assert (first[i], page[i]) == (want_first, want_page), i
