@@ -111,6 +111,36 @@ def probe_c3(torch, bh, steps, warmup):
             "hits_per_level": hit_counts}
 
 
+def route_c3(torch, bh, steps, warmup):
+    """§8f row 1: batched GET routing of C3's 16.8M GETs over the five level
+    runs (range check + filter probe + newest candidate + page index), all
+    outputs device-resident."""
+    from bloomhip import workloads as W
+    gets, levels = W.c3_runs()
+    runs = []
+    for lvl, keys, m in levels:
+        f = bh.BloomFilter(m)
+        f.set_batch_run(keys)
+        runs.append(f)
+    n = gets.size
+    dgets = torch.from_numpy(gets).cuda()
+    dc = torch.empty((len(runs), (n + 63) // 64), dtype=torch.int64, device="cuda")
+    df = torch.empty(n, dtype=torch.int32, device="cuda")
+    dp = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    for _ in range(warmup):
+        bh.route_gets(runs, dgets, cand=dc, first=df, page=dp, stream=s)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        bh.route_gets(runs, dgets, cand=dc, first=df, page=dp, stream=s)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    routed = int((df >= 0).sum().item())
+    return {"gkeys_s": round(n / (wall * 1e9), 3), "wall_ms": round(wall * 1e3, 4),
+            "keys_with_candidate": routed}
+
+
 def e2e_build(torch, bh, keys_np, m, reps=5):
     """Host keys (pinned) -> device -> filter -> host bitmap, wall clock."""
     import numpy as np
@@ -245,6 +275,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         log("probe C3 ...")
         extras["probe_c3"] = probe_c3(torch, bh, max(5, args.steps // 5), 2)
+        log("route C3 ...")
+        extras["route_c3"] = route_c3(torch, bh, max(5, args.steps // 5), 2)
         log("e2e ...")
         extras["e2e_build"] = e2e_build(torch, bh, keys, m)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

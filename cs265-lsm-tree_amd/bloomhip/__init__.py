@@ -56,7 +56,8 @@ EXPORTED_SYMBOLS = (
     "bloomhip_profile_read", "bloomhip_profile_reset", "bloomhip_trim", "bloomhip_host_positions",
     "bloomhip_gen_mt19937", "bloomhip_gen_glibc_rand", "bloomhip_gen_puts",
     "bloomhip_gen_workload", "bloomhip_set_batch_run", "bloomhip_set_run_meta",
-    "bloomhip_get_run_meta", "bloomhip_route_gets",
+    "bloomhip_get_run_meta", "bloomhip_route_gets", "bloomhip_save", "bloomhip_load",
+    "bloomhip_build_from_run_file",
 )
 
 
@@ -131,6 +132,10 @@ def _lib():
             "bloomhip_get_run_meta": (I, [P, P, SZ, ctypes.POINTER(SZ),
                                           ctypes.POINTER(ctypes.c_int32)]),
             "bloomhip_route_gets": (I, [ctypes.POINTER(P), I, P, SZ, SZ, I, P, P, P, I, P]),
+            "bloomhip_save": (I, [P, ctypes.c_char_p]),
+            "bloomhip_load": (I, [ctypes.c_char_p, I, ctypes.POINTER(P)]),
+            "bloomhip_build_from_run_file": (I, [ctypes.c_char_p, U64, ctypes.c_int64,
+                                                 ctypes.c_float, I, ctypes.POINTER(P)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -209,6 +214,38 @@ class BloomFilter:
         n = ctypes.c_uint64()
         _check(_lib().bloomhip_nwords(h, ctypes.byref(n)), "bloomhip_nwords")
         self.nwords = n.value
+
+    @classmethod
+    def _adopt(cls, h: ctypes.c_void_p, device: int) -> "BloomFilter":
+        self = cls.__new__(cls)
+        self._h = h
+        self.device = device
+        m, n = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(_lib().bloomhip_size(h, ctypes.byref(m)), "bloomhip_size")
+        _check(_lib().bloomhip_nwords(h, ctypes.byref(n)), "bloomhip_nwords")
+        self.m, self.nwords = m.value, n.value
+        return self
+
+    @classmethod
+    def load(cls, path: str, device: int = 0) -> "BloomFilter":
+        """A filter saved with save() (bloomhip_load)."""
+        h = ctypes.c_void_p()
+        _check(_lib().bloomhip_load(os.fsencode(path), device, ctypes.byref(h)), "bloomhip_load")
+        return cls._adopt(h, device)
+
+    @classmethod
+    def from_run_file(cls, path: str, n_entries: int, max_size: int, bits_per_entry: float,
+                      device: int = 0) -> "BloomFilter":
+        """Filter + run metadata rebuilt from a run file of entry_t records
+        (bloomhip_build_from_run_file)."""
+        h = ctypes.c_void_p()
+        _check(_lib().bloomhip_build_from_run_file(os.fsencode(path), n_entries, max_size,
+                                                   bits_per_entry, device, ctypes.byref(h)),
+               "bloomhip_build_from_run_file")
+        return cls._adopt(h, device)
+
+    def save(self, path: str) -> None:
+        _check(_lib().bloomhip_save(self._h, os.fsencode(path)), "bloomhip_save")
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

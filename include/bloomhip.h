@@ -152,6 +152,22 @@ int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const voi
                         uint64_t *cand_packed, int32_t *first_run, int32_t *page,
                         int out_on_device, void *stream);
 
+/* --- persistence beside the run -------------------------
+ * The reference keeps a run's entries in an mmap'd file (src/run.cpp:34-72)
+ * and its filter only in memory (src/run.h:11).  bloomhip_save writes the
+ * bitmap (dynamic_bitset blocks) and the run metadata to `path` (written to
+ * path.tmp, then renamed); bloomhip_load creates a filter on `device` from
+ * such a file (BLOOMHIP_EINVAL for a file that is not one, or is damaged:
+ * the file ends with an FNV-1a 64 checksum).  bloomhip_build_from_run_file
+ * maps a run file of entry_t {key, val} records (src/types.h:14-22), sizes
+ * the filter as Run::Run does (m = (long)((float)max_size * bpe),
+ * src/run.cpp:13-15) and builds it and the run metadata from its first
+ * n_entries records.  All synchronous. */
+int bloomhip_save(const bloomhip_filter *f, const char *path);
+int bloomhip_load(const char *path, int device, bloomhip_filter **out);
+int bloomhip_build_from_run_file(const char *path, uint64_t n_entries, int64_t max_size,
+                                 float bits_per_entry, int device, bloomhip_filter **out);
+
 /* Scalar compatibility entry points (one key; synchronous). */
 int bloomhip_set(bloomhip_filter *f, int32_t key);
 int bloomhip_is_set(const bloomhip_filter *f, int32_t key, int *hit_out);

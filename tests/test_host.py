@@ -145,3 +145,15 @@ def test_c1_run_is_sorted_distinct_prefix():
     run, m = W.c1_run()
     assert m == 512_000 and run.shape == (51_200, 2)
     assert (np.diff(run[:, 0].astype(np.int64)) > 0).all()
+
+
+def test_load_of_a_non_filter_file_fails_before_touching_the_gpu(tmp_path):
+    """bloomhip_load validates the file on the host first (no GPU needed)."""
+    import ctypes
+    p = tmp_path / "junk.bloom"
+    p.write_bytes(b"not a filter at all" * 10)
+    h = ctypes.c_void_p()
+    L = bh._lib()
+    assert L.bloomhip_load(str(p).encode(), 0, ctypes.byref(h)) == bh.EINVAL
+    assert L.bloomhip_load(str(tmp_path / "none").encode(), 0, ctypes.byref(h)) == -5  # EIO
+    assert not h.value
