@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = (
     "bloomhip_gen_mt19937", "bloomhip_gen_glibc_rand", "bloomhip_gen_puts",
     "bloomhip_gen_workload", "bloomhip_set_batch_run", "bloomhip_set_run_meta",
     "bloomhip_get_run_meta", "bloomhip_route_gets", "bloomhip_save", "bloomhip_load",
-    "bloomhip_build_from_run_file",
+    "bloomhip_build_from_run_file", "bloomhip_compact",
 )
 
 
@@ -132,6 +132,8 @@ def _lib():
             "bloomhip_get_run_meta": (I, [P, P, SZ, ctypes.POINTER(SZ),
                                           ctypes.POINTER(ctypes.c_int32)]),
             "bloomhip_route_gets": (I, [ctypes.POINTER(P), I, P, SZ, SZ, I, P, P, P, I, P]),
+            "bloomhip_compact": (I, [ctypes.POINTER(P), P, I, I, I, P, ctypes.POINTER(SZ), I, P,
+                                     I, P]),
             "bloomhip_save": (I, [P, ctypes.c_char_p]),
             "bloomhip_load": (I, [ctypes.c_char_p, I, ctypes.POINTER(P)]),
             "bloomhip_build_from_run_file": (I, [ctypes.c_char_p, U64, ctypes.c_int64,
@@ -410,6 +412,35 @@ def route_gets(runs: Sequence[BloomFilter], keys, n: int | None = None, stride: 
                                       outs[2][0], out_dev, _stream_ptr(stream)),
            "bloomhip_route_gets")
     return cand, first, page
+
+
+def compact(runs, drop_tombstones: bool = False, filter: BloomFilter | None = None,
+            device: int = 0, out=None, stream=None):
+    """Compaction (bloomhip_compact): runs = entry_t arrays (int32 [n, 2] numpy
+    arrays or device tensors), newest first.  Returns the merged run (a
+    [n_out, 2] int32 array, or the first n_out rows of `out` when given);
+    builds `filter` (and its run metadata) from the merged keys when given."""
+    nr = len(runs)
+    keeps = [_ptr_of(r) for r in runs]
+    ons = {k[1] for k in keeps}
+    if len(ons) > 1:
+        raise ValueError("runs must be all host or all device buffers")
+    on_dev = ons.pop() if ons else 0
+    sizes = [(k[2].nbytes if isinstance(k[2], np.ndarray) else k[2].numel() * k[2].element_size())
+             // 8 for k in keeps]
+    total = sum(sizes)
+    if out is None:
+        out = np.empty((max(total, 1), 2), dtype=np.int32)
+    optr, out_dev, okeep = _ptr_of(out)
+    arr = (ctypes.c_void_p * max(nr, 1))(*[k[0] for k in keeps])
+    ns = (ctypes.c_size_t * max(nr, 1))(*sizes)
+    n_out = ctypes.c_size_t()
+    _check(_lib().bloomhip_compact(arr, ns, nr, on_dev, 1 if drop_tombstones else 0, optr,
+                                   ctypes.byref(n_out), out_dev,
+                                   filter.handle if filter is not None else None,
+                                   filter.device if filter is not None else device,
+                                   _stream_ptr(stream)), "bloomhip_compact")
+    return out[:n_out.value]
 
 
 # --- workload streams (generator/generator.c restatement) --------------------

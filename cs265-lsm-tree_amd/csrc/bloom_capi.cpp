@@ -21,6 +21,7 @@
 
 #include "../../include/bloomhip.h"
 #include "bloom_kernels.h"
+#include "bloom_merge.h"
 
 using namespace bloomhip;
 
@@ -161,6 +162,12 @@ struct Workspace {
     size_t res_bytes = 0;
     uint16_t *slots = nullptr;  // partitioned probe: sorted slot per (key, hash)
     size_t slots_bytes = 0;
+    void *mbuf[2] = {nullptr, nullptr};  // compaction: merge rounds ping-pong
+    size_t mbuf_bytes[2] = {0, 0};
+    uint64_t *msplit = nullptr;  // compaction: merge-path splits
+    size_t msplit_bytes = 0;
+    uint32_t *mcount = nullptr;  // compaction: block counts / offsets
+    size_t mcount_bytes = 0;
 };
 
 std::mutex g_ws_mu;
@@ -918,10 +925,103 @@ int bloomhip_trim(void) {
         std::lock_guard<std::mutex> wl(w->mu);
         DeviceGuard g(kv.first.first);
         (void)hipStreamSynchronize(kv.first.second);
-        for (void *p : {(void *)w->pos, (void *)w->runs, (void *)w->res, (void *)w->slots})
+        for (void *p : {(void *)w->pos, (void *)w->runs, (void *)w->res, (void *)w->slots,
+                        w->mbuf[0], w->mbuf[1], (void *)w->msplit, (void *)w->mcount})
             if (p) (void)hipFree(p);
     }
     g_ws.clear();
+    return BLOOMHIP_OK;
+}
+
+int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
+                     int runs_on_device, int drop_tombstones, void *out_entries, size_t *n_out,
+                     int out_on_device, bloomhip_filter *f, int device, void *stream) {
+    g_last_error.clear();
+    if (nruns < 0 || (nruns && (!runs || !nentries)) || !n_out || (f && f->device != device))
+        return BLOOMHIP_EINVAL;
+    uint64_t total = 0;
+    for (int r = 0; r < nruns; r++) {
+        if (nentries[r] && !runs[r]) return BLOOMHIP_EINVAL;
+        total += nentries[r];
+    }
+    if (total >= 0xFFFFFFFFull) return BLOOMHIP_ERANGE;  // 32-bit block offsets
+    if (total && !out_entries) return BLOOMHIP_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return BLOOMHIP_ENODEV;
+    if (device < 0 || device >= ndev) return BLOOMHIP_EINVAL;
+    DeviceGuard g(device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const void *dout = nullptr;
+    uint64_t kept = 0;
+    {
+        Workspace *w = workspace_for(device, s);
+        std::lock_guard<std::mutex> wl(w->mu);
+        const size_t bytes = std::max<uint64_t>(total, 1) * 8;
+        for (int i = 0; i < 2; i++) HIP_TRY(grow_touched(&w->mbuf[i], &w->mbuf_bytes[i], bytes, s));
+        HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->msplit), &w->msplit_bytes,
+                             merge_split_words(total) * 8, s));
+        HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->mcount), &w->mcount_bytes,
+                             compact_count_words(total) * 4 + 4, s));
+        // the runs, newest first; host runs are staged into mbuf[0]
+        std::vector<std::pair<const char *, uint64_t>> list;
+        uint64_t off = 0;
+        for (int r = 0; r < nruns; r++) {
+            if (!nentries[r]) continue;
+            if (runs_on_device) {
+                list.push_back({static_cast<const char *>(runs[r]), nentries[r]});
+            } else {
+                char *dst = static_cast<char *>(w->mbuf[0]) + off * 8;
+                HIP_TRY(hipMemcpyAsync(dst, runs[r], nentries[r] * 8, hipMemcpyHostToDevice, s));
+                list.push_back({dst, nentries[r]});
+                off += nentries[r];
+            }
+        }
+        // pairwise merge rounds, the left (newer) input winning ties; round
+        // outputs alternate between the two buffers, never the round's input
+        int dst_buf = runs_on_device ? 0 : 1;
+        while (list.size() > 1) {
+            std::vector<std::pair<const char *, uint64_t>> next;
+            char *base = static_cast<char *>(w->mbuf[dst_buf]);
+            uint64_t o = 0;
+            for (size_t i = 0; i < list.size(); i += 2) {
+                char *dst = base + o * 8;
+                if (i + 1 < list.size()) {
+                    hipError_t e = launch_merge2(list[i].first, list[i].second, list[i + 1].first,
+                                                 list[i + 1].second, dst, w->msplit, s);
+                    if (e != hipSuccess) return fail_hip(e, "merge launch");
+                    next.push_back({dst, list[i].second + list[i + 1].second});
+                } else {
+                    HIP_TRY(hipMemcpyAsync(dst, list[i].first, list[i].second * 8,
+                                           hipMemcpyDeviceToDevice, s));
+                    next.push_back({dst, list[i].second});
+                }
+                o += next.back().second;
+            }
+            list.swap(next);
+            dst_buf ^= 1;
+        }
+        // newest entry per key, tombstones dropped on request
+        const char *merged = list.empty() ? nullptr : list[0].first;
+        void *dst = out_on_device ? out_entries : w->mbuf[merged == w->mbuf[0] ? 1 : 0];
+        if (merged) {
+            hipError_t e = launch_dedup(merged, total, drop_tombstones, dst, w->mcount, s);
+            if (e != hipSuccess) return fail_hip(e, "dedup launch");
+            uint32_t cnt = 0;
+            HIP_TRY(hipMemcpyAsync(&cnt, w->mcount + compact_count_words(total) - 1, 4,
+                                   hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            kept = cnt;
+        }
+        dout = dst;
+    }
+    *n_out = (size_t)kept;
+    if (f) {
+        int rc = bloomhip_set_batch_run(f, dout, (size_t)kept, 8, 1, stream);
+        if (rc) return rc;
+    }
+    if (!out_on_device && kept)
+        HIP_TRY(hipMemcpyAsync(out_entries, dout, kept * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
     return BLOOMHIP_OK;
 }
 

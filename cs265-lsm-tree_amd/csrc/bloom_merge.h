@@ -1,0 +1,22 @@
+// bloom_merge.h — compaction kernels; see bloom_merge.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bloomhip {
+
+// Stable merge of two key-sorted entry_t arrays (a wins ties) into out
+// (na + nb entries).  split_ws: merge_split_words(na + nb) u64.
+hipError_t launch_merge2(const void *a, uint64_t na, const void *b, uint64_t nb, void *out,
+                         uint64_t *split_ws, hipStream_t stream);
+uint64_t merge_split_words(uint64_t total);
+
+// Keeps the first entry of each key of a key-sorted array (dropping entries
+// whose value is VAL_TOMBSTONE when drop_tombstones), packed into out; the
+// kept count lands in counts_ws[ceil(n / tile)] (compact_count_words(n) u32).
+hipError_t launch_dedup(const void *in, uint64_t n, int drop_tombstones, void *out,
+                        uint32_t *counts_ws, hipStream_t stream);
+uint64_t compact_count_words(uint64_t n);
+
+}  // namespace bloomhip

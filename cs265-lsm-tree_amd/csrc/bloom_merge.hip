@@ -1,0 +1,216 @@
+// bloom_merge.hip — SURVEY §8f row 3: the compaction that produces a run's
+// keys, fused with that run's filter build.
+//
+// Reference: MergeContext (src/merge.h:8-37, src/merge.cpp:6-39) pops the
+// smallest (key, precedence) head of k sorted runs — precedence = the order
+// runs were added, newest first (LSMTree::merge_down iterates a level's
+// runs front to back, src/lsm_tree.cpp:74-76, and runs are emplace_front'ed,
+// :78,125) — and releases only the newest entry of each key; merge_down drops
+// entries whose value is VAL_TOMBSTONE when writing the last level
+// (src/lsm_tree.cpp:81-88).  Run::put then sets the filter bits and fences.
+//
+// On the GPU: a tree of stable 2-way merges (merge path: per 2048-output tile
+// a binary search on the cross diagonal picks each input's share, the tile is
+// staged in LDS and each lane merges 8 outputs), left input always the newer,
+// so equal keys come out newest first; then one compaction pass keeps the
+// first entry of each key (dropping tombstones on request) with a block scan
+// and a scan over the block counts.  Every pass streams entries through HBM
+// with coalesced 16-B accesses; the filter build runs on the merged keys in
+// place (stride 8).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bloom_merge.h"
+
+namespace bloomhip {
+namespace {
+
+constexpr int kMergeBlock = 256;
+constexpr int kMergeIpt = 8;                          // outputs per lane
+constexpr int kMergeTile = kMergeBlock * kMergeIpt;  // outputs per workgroup
+constexpr int32_t kTombstone = INT32_MIN;            // VAL_TOMBSTONE, src/types.h:12
+
+struct Entry {
+    int32_t key, val;
+};
+
+// Number of A entries among the first d outputs of the stable merge (A wins
+// ties): the largest i with A[i-1] before B[d-i].
+template <typename GetA, typename GetB>
+__device__ __forceinline__ uint64_t merge_path(GetA a_key, uint64_t na, GetB b_key, uint64_t nb,
+                                               uint64_t d) {
+    uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a_key(mid) <= b_key(d - 1 - mid)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_merge_split(const Entry *__restrict__ a, uint64_t na,
+                              const Entry *__restrict__ b, uint64_t nb, uint64_t ntiles,
+                              uint64_t *__restrict__ split) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const uint64_t d = min(t * (uint64_t)kMergeTile, na + nb);
+    split[t] = merge_path([&](uint64_t i) { return a[i].key; }, na,
+                          [&](uint64_t j) { return b[j].key; }, nb, d);
+}
+
+__global__ void __launch_bounds__(kMergeBlock) k_merge_tile(const Entry *__restrict__ a,
+                                                            uint64_t na,
+                                                            const Entry *__restrict__ b,
+                                                            uint64_t nb,
+                                                            const uint64_t *__restrict__ split,
+                                                            Entry *__restrict__ out) {
+    __shared__ Entry s_in[kMergeTile];
+    __shared__ Entry s_out[kMergeTile];
+    const uint64_t t = blockIdx.x;
+    const uint64_t d0 = t * kMergeTile, d1 = min(d0 + kMergeTile, na + nb);
+    const uint64_t a0 = split[t], a1 = split[t + 1];
+    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
+    const int ta = (int)(a1 - a0), tb = (int)(b1 - b0);
+    for (int i = threadIdx.x; i < ta; i += kMergeBlock) s_in[i] = a[a0 + i];
+    for (int i = threadIdx.x; i < tb; i += kMergeBlock) s_in[ta + i] = b[b0 + i];
+    __syncthreads();
+    const int d = threadIdx.x * kMergeIpt;
+    const int total = ta + tb;
+    if (d < total) {
+        const Entry *sa = s_in, *sb = s_in + ta;
+        int ia = (int)merge_path([&](uint64_t i) { return sa[i].key; }, (uint64_t)ta,
+                                 [&](uint64_t j) { return sb[j].key; }, (uint64_t)tb, (uint64_t)d);
+        int ib = d - ia;
+        const int n = min(kMergeIpt, total - d);
+        for (int k = 0; k < n; k++) {
+            const bool take_a = ia < ta && (ib >= tb || sa[ia].key <= sb[ib].key);
+            s_out[d + k] = take_a ? sa[ia++] : sb[ib++];
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < total; i += kMergeBlock) out[d0 + i] = s_out[i];
+}
+
+// Keep entry i when it is the first (newest) of its key, and not a dropped
+// tombstone.
+__device__ __forceinline__ bool keep(const Entry *e, uint64_t i, int drop_tombstones) {
+    const Entry x = e[i];
+    if (i > 0 && e[i - 1].key == x.key) return false;
+    return !(drop_tombstones && x.val == kTombstone);
+}
+
+constexpr int kCompactBlock = 256;
+constexpr int kCompactIpt = 8;
+constexpr int kCompactTile = kCompactBlock * kCompactIpt;
+
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *s_w,
+                                                         uint32_t *total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+    for (int w = 0; w < (int)(blockDim.x / 64); w++) {
+        if (w < wave) base += s_w[w];
+        all += s_w[w];
+    }
+    __syncthreads();
+    if (total) *total = all;
+    return base + incl - v;
+}
+
+__global__ void __launch_bounds__(kCompactBlock) k_compact_count(const Entry *__restrict__ e,
+                                                                 uint64_t n, int drop,
+                                                                 uint32_t *__restrict__ counts) {
+    __shared__ uint32_t s_w[kCompactBlock / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kCompactTile + (uint64_t)threadIdx.x * kCompactIpt;
+    uint32_t c = 0;
+    for (int k = 0; k < kCompactIpt; k++)
+        if (base + k < n && keep(e, base + k, drop)) c++;
+    uint32_t total;
+    (void)block_exclusive_scan(c, s_w, &total);
+    if (threadIdx.x == 0) counts[blockIdx.x] = total;
+}
+
+// Exclusive scan of the block counts in place (one workgroup), total in
+// counts[nblocks].
+__global__ void __launch_bounds__(1024) k_scan_counts(uint32_t *__restrict__ counts,
+                                                      uint64_t nblocks) {
+    __shared__ uint32_t s_w[1024 / 64];
+    __shared__ uint64_t s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint64_t b0 = 0; b0 < nblocks; b0 += 1024) {
+        const uint64_t i = b0 + threadIdx.x;
+        const uint32_t v = i < nblocks ? counts[i] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(v, s_w, &total);
+        if (i < nblocks) counts[i] = (uint32_t)(s_carry + ex);
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) counts[nblocks] = (uint32_t)s_carry;
+}
+
+__global__ void __launch_bounds__(kCompactBlock) k_compact_write(
+    const Entry *__restrict__ e, uint64_t n, int drop, const uint32_t *__restrict__ offsets,
+    Entry *__restrict__ out) {
+    __shared__ uint32_t s_w[kCompactBlock / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kCompactTile + (uint64_t)threadIdx.x * kCompactIpt;
+    bool kf[kCompactIpt];
+    uint32_t c = 0;
+    for (int k = 0; k < kCompactIpt; k++) {
+        kf[k] = base + k < n && keep(e, base + k, drop);
+        c += kf[k];
+    }
+    uint32_t pos = offsets[blockIdx.x] + block_exclusive_scan(c, s_w, nullptr);
+    for (int k = 0; k < kCompactIpt; k++)
+        if (kf[k]) out[pos++] = e[base + k];
+}
+
+}  // namespace
+
+hipError_t launch_merge2(const void *a, uint64_t na, const void *b, uint64_t nb, void *out,
+                         uint64_t *split_ws, hipStream_t stream) {
+    const uint64_t total = na + nb;
+    if (total == 0) return hipSuccess;
+    const uint64_t ntiles = (total + kMergeTile - 1) / kMergeTile;
+    const Entry *ea = reinterpret_cast<const Entry *>(a);
+    const Entry *eb = reinterpret_cast<const Entry *>(b);
+    k_merge_split<<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, stream>>>(ea, na, eb, nb, ntiles,
+                                                                          split_ws);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_merge_tile<<<(unsigned)ntiles, kMergeBlock, 0, stream>>>(ea, na, eb, nb, split_ws,
+                                                               reinterpret_cast<Entry *>(out));
+    return hipGetLastError();
+}
+
+uint64_t merge_split_words(uint64_t total) { return total / kMergeTile + 2; }
+uint64_t compact_count_words(uint64_t n) { return (n + kCompactTile - 1) / kCompactTile + 1; }
+
+hipError_t launch_dedup(const void *in, uint64_t n, int drop_tombstones, void *out,
+                        uint32_t *counts_ws, hipStream_t stream) {
+    const uint64_t nblocks = (n + kCompactTile - 1) / kCompactTile;
+    const Entry *e = reinterpret_cast<const Entry *>(in);
+    if (nblocks) {
+        k_compact_count<<<(unsigned)nblocks, kCompactBlock, 0, stream>>>(e, n, drop_tombstones,
+                                                                          counts_ws);
+        hipError_t err = hipGetLastError();
+        if (err != hipSuccess) return err;
+    }
+    k_scan_counts<<<1, 1024, 0, stream>>>(counts_ws, nblocks);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess || nblocks == 0) return err;
+    k_compact_write<<<(unsigned)nblocks, kCompactBlock, 0, stream>>>(
+        e, n, drop_tombstones, counts_ws, reinterpret_cast<Entry *>(out));
+    return hipGetLastError();
+}
+
+}  // namespace bloomhip

@@ -168,6 +168,24 @@ int bloomhip_load(const char *path, int device, bloomhip_filter **out);
 int bloomhip_build_from_run_file(const char *path, uint64_t n_entries, int64_t max_size,
                                  float bits_per_entry, int device, bloomhip_filter **out);
 
+/* --- compaction fused with the new run's filter build ----
+ * LSMTree::merge_down (src/lsm_tree.cpp:48-95) through MergeContext
+ * (src/merge.cpp:6-39): a k-way merge of nruns key-sorted runs of entry_t
+ * {key, val} records (src/types.h:14-22), runs[0] the newest (precedence 0),
+ * releasing for each distinct key only the newest run's entry; with
+ * drop_tombstones (merging into the last level, src/lsm_tree.cpp:84-86)
+ * entries whose val is VAL_TOMBSTONE (INT32_MIN) are dropped.  The merged run
+ * (ascending keys) goes to out_entries (capacity: the sum of nentries; must
+ * not alias an input) and its length to *n_out.  When f is not NULL the new
+ * run's filter and metadata are built from the merged keys in the same call
+ * (bloomhip_set_batch_run on the device copy).  Runs and output are host
+ * buffers unless runs_on_device / out_on_device; everything runs on
+ * `device` (f's device when given).  Synchronous (the output length is
+ * returned). */
+int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
+                     int runs_on_device, int drop_tombstones, void *out_entries, size_t *n_out,
+                     int out_on_device, bloomhip_filter *f, int device, void *stream);
+
 /* Scalar compatibility entry points (one key; synchronous). */
 int bloomhip_set(bloomhip_filter *f, int32_t key);
 int bloomhip_is_set(const bloomhip_filter *f, int32_t key, int *hit_out);

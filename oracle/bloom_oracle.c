@@ -214,3 +214,38 @@ int bo_route(int nruns, const uint64_t *const *words, const uint64_t *ms,
     }
     return 0;
 }
+
+/* ---- §8f row 3: compaction (LSMTree::merge_down + MergeContext) ----------
+ *
+ * runs[r] is a key-sorted array of entry_t {key, val} (int32 pairs,
+ * src/types.h:14-22), runs[0] the newest.  MergeContext::add gives each
+ * non-empty run precedence = its position (src/merge.cpp:6-15); next() pops
+ * the smallest (head key, precedence), advances every run whose head has
+ * that key, and releases the popped entry (:17-33).  merge_down drops
+ * entries whose val is VAL_TOMBSTONE when writing the last level
+ * (src/lsm_tree.cpp:81-88).  Returns the number of entries written to out.
+ */
+size_t bo_compact(const int32_t *const *runs, const size_t *n, int nruns, int drop_tombstones,
+                  int32_t *out) {
+    size_t idx[256] = {0};
+    size_t w = 0;
+    if (nruns > 256) return 0;
+    for (;;) {
+        int best = -1;
+        for (int r = 0; r < nruns; r++) {
+            if (idx[r] >= n[r]) continue;
+            if (best < 0 || runs[r][2 * idx[r]] < runs[best][2 * idx[best]]) best = r;
+        }
+        if (best < 0) break;
+        const int32_t key = runs[best][2 * idx[best]];
+        const int32_t val = runs[best][2 * idx[best] + 1];
+        for (int r = 0; r < nruns; r++)
+            while (idx[r] < n[r] && runs[r][2 * idx[r]] == key) idx[r]++;
+        if (!(drop_tombstones && val == INT32_MIN)) {
+            out[2 * w] = key;
+            out[2 * w + 1] = val;
+            w++;
+        }
+    }
+    return w;
+}

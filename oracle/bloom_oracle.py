@@ -148,6 +148,8 @@ class COracle:
         L.bo_route.argtypes = [ctypes.c_int, P, P, P, P, P, P, ctypes.c_size_t, ctypes.c_size_t,
                                P, P, P]
         L.bo_route.restype = ctypes.c_int
+        L.bo_compact.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P]
+        L.bo_compact.restype = ctypes.c_size_t
         self.L = L
 
     def m_bits(self, max_size: int, bpe: float) -> int:
@@ -240,3 +242,17 @@ COracle.run_meta = lambda self, keys, stride=4, n=None: _run_meta(self.L, keys, 
 COracle.run_meta.__doc__ = "(fences, max_key) of a run written in this key order (src/run.cpp:158-174)."
 COracle.route = lambda self, runs, keys, stride=4: _route(self.L, runs, keys, stride)
 COracle.route.__doc__ = _route.__doc__
+
+
+def _compact(L, runs, drop_tombstones: bool = False):
+    """Merged run (int32 [n, 2]) of entry_t runs, newest first."""
+    keep = [np.ascontiguousarray(r, dtype=np.int32).reshape(-1, 2) for r in runs]
+    R = (ctypes.c_void_p * max(1, len(keep)))(*[k.ctypes.data for k in keep])
+    ns = np.array([k.shape[0] for k in keep] or [0], dtype=np.uint64)
+    out = np.empty((max(1, int(ns.sum())), 2), dtype=np.int32)
+    w = L.bo_compact(R, ns.ctypes.data, len(keep), 1 if drop_tombstones else 0, out.ctypes.data)
+    return out[:w]
+
+
+COracle.compact = lambda self, runs, drop_tombstones=False: _compact(self.L, runs, drop_tombstones)
+COracle.compact.__doc__ = _compact.__doc__

@@ -1,0 +1,69 @@
+"""GPU parity of §8f row 3: compaction (k-way merge, newest wins, optional
+tombstone drop) fused with the new run's filter + metadata build, against
+the oracle's MergeContext restatement (oracle/bloom_oracle.c bo_compact)."""
+import numpy as np
+import pytest
+
+import bloomhip as bh
+
+pytestmark = pytest.mark.gpu
+TOMB = np.iinfo(np.int32).min
+
+
+def make_runs(sizes, key_range, seed, tomb_frac=0.05):
+    rng = np.random.default_rng(seed)
+    runs = []
+    for n in sizes:
+        keys = np.unique(rng.integers(-key_range, key_range, size=n, dtype=np.int64)
+                         .astype(np.int32))
+        vals = rng.integers(-2**31 + 1, 2**31, size=keys.size, dtype=np.int64).astype(np.int32)
+        vals[rng.random(keys.size) < tomb_frac] = TOMB
+        runs.append(np.ascontiguousarray(np.stack([keys, vals], axis=1)))
+    return runs
+
+
+@pytest.mark.parametrize("sizes", [[0], [1], [5000], [3000, 0, 7000], [1, 1, 1, 1, 1],
+                                   [10_000] * 7, [2049, 2047, 4096, 1]])
+@pytest.mark.parametrize("drop", [False, True])
+def test_compact_matches_oracle(coracle, sizes, drop):
+    runs = make_runs(sizes, 20_000, len(sizes) * 7 + sum(sizes) % 97)
+    got = bh.compact(runs, drop_tombstones=drop)
+    want = coracle.compact(runs, drop)
+    assert np.array_equal(got, want)
+
+
+def test_compact_extreme_keys_and_all_duplicates(coracle):
+    ext = np.array([[TOMB, 1], [-1, 2], [0, 3], [2**31 - 1, 4]], dtype=np.int32)
+    runs = [ext.copy(), ext.copy(), ext.copy()]
+    runs[1][:, 1] = 9
+    runs[0][2, 1] = TOMB
+    for drop in (False, True):
+        assert np.array_equal(bh.compact(runs, drop), coracle.compact(runs, drop))
+
+
+def test_compact_builds_the_new_runs_filter(coracle):
+    runs = make_runs([400_000, 250_000, 120_000, 60_000], 2**30, 3)
+    total = sum(r.shape[0] for r in runs)
+    m = bh.m_bits(total, 10.0)
+    f = bh.BloomFilter(m)
+    got = bh.compact(runs, drop_tombstones=True, filter=f)
+    want = coracle.compact(runs, True)
+    assert np.array_equal(got, want)
+    assert (f.words() == coracle.build(m, want[:, 0].copy())).all()
+    fences, mk = f.run_meta()
+    wf, wmk = coracle.run_meta(want[:, 0].copy())
+    assert np.array_equal(fences, wf) and mk == wmk
+
+
+def test_compact_device_buffers(coracle):
+    torch = pytest.importorskip("torch")
+    runs = make_runs([300_001, 100_000, 7], 2**31 - 1, 5)
+    druns = [torch.from_numpy(r).cuda() for r in runs]
+    total = sum(r.shape[0] for r in runs)
+    dout = torch.empty((total, 2), dtype=torch.int32, device="cuda")
+    f = bh.BloomFilter(bh.m_bits(total, 8.0))
+    got = bh.compact(druns, drop_tombstones=False, filter=f, out=dout)
+    torch.cuda.synchronize()
+    want = coracle.compact(runs, False)
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()

@@ -137,3 +137,25 @@ def test_route_restatement_matches_python_loops(coracle):
                 want_first = r
                 want_page = bisect.bisect_right(list(fences), k) - 1
         assert (first[i], page[i]) == (want_first, want_page), i
+
+
+def test_compact_restatement_matches_python(coracle):
+    """bo_compact against a dict-based restatement: newest run wins per key,
+    tombstones dropped only when asked (src/merge.cpp:6-39,
+    src/lsm_tree.cpp:81-88)."""
+    rng = np.random.default_rng(8)
+    runs = []
+    for n in (0, 50, 400, 1000, 3):
+        keys = np.unique(rng.integers(-300, 300, size=n, dtype=np.int64).astype(np.int32))
+        vals = rng.integers(-5, 5, size=keys.size, dtype=np.int64).astype(np.int32)
+        vals[vals == -5] = np.iinfo(np.int32).min           # tombstones
+        runs.append(np.stack([keys, vals], axis=1))
+    for drop in (False, True):
+        newest = {}
+        for r in reversed(runs):                            # oldest first, newer overwrite
+            for k, v in r.tolist():
+                newest[k] = v
+        want = [(k, v) for k, v in sorted(newest.items())
+                if not (drop and v == np.iinfo(np.int32).min)]
+        got = coracle.compact(runs, drop)
+        assert [tuple(x) for x in got.tolist()] == want
