@@ -98,7 +98,8 @@ def probe_c3(torch, bh, steps, warmup):
     torch.cuda.synchronize()
     prof = f0.profile_read()
     f0.profile(False)
-    kms = sum(v["ms"] for k, v in prof.items() if k in ("k_probe", "probe_partitioned")) / steps
+    kms = sum(v["ms"] for k, v in prof.items()
+              if k in ("k_probe", "probe_partitioned", "k_probe_lds", "probe_stacked")) / steps
     hits = dout.cpu().numpy().view("uint64")
     import numpy as np
     hit_counts = [int(np.unpackbits(hits[j].view(np.uint8)).sum()) for j in range(len(filters))]

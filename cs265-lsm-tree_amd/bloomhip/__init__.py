@@ -41,9 +41,10 @@ PROBE_AUTO = 0
 PROBE_GATHER = 1
 PROBE_PARTITION = 2
 PROBE_LDS = 3
+PROBE_STACKED = 4
 STRATEGY_NAMES = {BUILD_AUTO: "auto", BUILD_ATOMIC: "atomic", BUILD_LDS: "lds",
                   BUILD_PARTITION: "partition"}
-PROF_SLOTS = 9
+PROF_SLOTS = 10
 
 # Every symbol include/bloomhip.h and include/bloomhip_workload.h declare.
 EXPORTED_SYMBOLS = (

@@ -15,6 +15,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <utility>
 #include <vector>
@@ -70,10 +71,11 @@ enum ProfSlot {
     SLOT_PROBE_PART = 6,
     SLOT_COPY = 7,
     SLOT_PROBE_LDS = 8,
+    SLOT_PROBE_STACK = 9,
 };
 const char *kSlotNames[BLOOMHIP_PROF_SLOTS] = {
     "clear(memset)", "k_build_atomic", "k_build_lds",       "k_part_bin", "k_part_apply",
-    "k_probe",       "probe_partitioned", "copy",           "k_probe_lds",
+    "k_probe",       "probe_partitioned", "copy",           "k_probe_lds",  "probe_stacked",
 };
 
 struct PendingTiming {
@@ -280,12 +282,10 @@ int strategy_supported(const bloomhip_filter *f, int strategy) {
     }
 }
 
-// Geometry of a partition pass over n keys for filter size m, with the
-// position/run buffers of `w` grown to fit.
-int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
-                        PartitionWorkspace *out) {
-    PartitionWorkspace ws{};
-    if (!plan_segments(m, device_cu_count(), &ws)) return BLOOMHIP_ERANGE;
+// A partition pass over n keys with the segment geometry in *ws (from
+// plan_segments / plan_stack): the position/run buffers of `w` grown to fit.
+int partition_buffers(Workspace *w, size_t n, hipStream_t s, PartitionWorkspace *ws_inout) {
+    PartitionWorkspace ws = *ws_inout;
     ws.ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->pos), &w->pos_bytes,
                          ws.ntiles * (size_t)kPartTilePos * 4, s));
@@ -294,7 +294,26 @@ int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
     ws.pos = w->pos;
     ws.run_rows = w->runs;
     ws.run_starts = w->runs + table;
+    *ws_inout = ws;
+    return BLOOMHIP_OK;
+}
+
+// Geometry of a partition pass over n keys for filter size m, with the
+// position/run buffers of `w` grown to fit.
+int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
+                        PartitionWorkspace *out) {
+    PartitionWorkspace ws{};
+    if (!plan_segments(m, device_cu_count(), &ws)) return BLOOMHIP_ERANGE;
     *out = ws;
+    return partition_buffers(w, n, s, out);
+}
+
+// The partitioned probe's result bytes and slots, grown to fit ws.
+int probe_buffers(Workspace *w, const PartitionWorkspace &ws, hipStream_t s) {
+    HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->res), &w->res_bytes,
+                         ws.ntiles * (size_t)kPartTilePos, s));
+    HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->slots), &w->slots_bytes,
+                         ws.ntiles * 3 * kPartTileKeys * sizeof(uint16_t), s));
     return BLOOMHIP_OK;
 }
 
@@ -312,11 +331,12 @@ int probe_kind(const bloomhip_filter *f, int owner_strategy, size_t n) {
     if (st == BLOOMHIP_PROBE_LDS)
         return lds_probe_able(f) ? BLOOMHIP_PROBE_LDS : BLOOMHIP_PROBE_GATHER;
     if (st == BLOOMHIP_PROBE_GATHER) return BLOOMHIP_PROBE_GATHER;
-    // AUTO (tools/probe_sweep.py): LDS-sized filters from LDS
+    // AUTO (and STACKED for a filter no stack took) (tools/probe_sweep.py): LDS-sized filters from LDS
     // once the batch amortises the staging; gathers while the filter mostly
     // hits in L2 / MALL; beyond that the partitioned probe.
     if (lds_probe_able(f) && n >= kProbeLdsMinKeys) return BLOOMHIP_PROBE_LDS;
-    if (partition_able(f) && (f->m + 7) / 8 > kProbeGatherMaxBytes && n >= kProbePartitionMinKeys)
+    if (partition_able(f) && (f->m + 7) / 8 > kProbeGatherMaxBytes &&
+        n >= kProbePartitionMinKeys)
         return BLOOMHIP_PROBE_PARTITION;
     return BLOOMHIP_PROBE_GATHER;
 }
@@ -623,16 +643,99 @@ int bloomhip_get_run_meta(const bloomhip_filter *f, int32_t *fences, size_t cap,
 
 namespace {
 
+// Device time of probing one filter alone, and of one stacked pass, in us
+// per 2^24 keys on MI355X (C3's level filters, tools/probe_sweep.py): what
+// AUTO weighs before stacking a group.
+constexpr double kCostLds = 70, kCostGatherL2 = 125, kCostGatherFar = 530, kCostPartition = 250,
+                 kCostStacked = 230;
+
+double probe_cost_alone(const bloomhip_filter *f, size_t n) {
+    switch (probe_kind(f, BLOOMHIP_PROBE_AUTO, n)) {
+        case BLOOMHIP_PROBE_LDS: return kCostLds;
+        case BLOOMHIP_PROBE_PARTITION: return kCostPartition;
+        default: return (f->m + 7) / 8 <= kProbeGatherMaxBytes ? kCostGatherL2 : kCostGatherFar;
+    }
+}
+
+int effective_probe_strategy(const bloomhip_filter *f, int owner_strategy) {
+    return f->probe_strategy != BLOOMHIP_PROBE_AUTO ? f->probe_strategy : owner_strategy;
+}
+
+// Stacked probes (BLOOMHIP_PROBE_STACKED, kernels.h StackTable) for the
+// groups of filters that take one; marks their rows in `done`.  Largest
+// filter first: its group is every not-yet-taken filter whose m divides its
+// m (largest first, <= kMaxStack).  A group with an explicit STACKED member
+// always runs; an AUTO group runs when it beats its members' own probes.
+int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int nf,
+                 const KeySpan &ks, size_t n, uint64_t *dout, hipStream_t s,
+                 std::vector<char> &done) {
+    std::vector<int> cand;
+    for (int j = 0; j < nf; j++) {
+        const int st = effective_probe_strategy(filters[j], f0->probe_strategy);
+        if (filters[j]->mp.fast && (st == BLOOMHIP_PROBE_AUTO || st == BLOOMHIP_PROBE_STACKED))
+            cand.push_back(j);
+    }
+    std::stable_sort(cand.begin(), cand.end(),
+                     [&](int a, int b) { return filters[a]->m > filters[b]->m; });
+    const int ncu = device_cu_count();
+    const size_t nw = (n + 63) / 64;
+    for (size_t a = 0; a < cand.size(); a++) {
+        const int h = cand[a];
+        if (done[h]) continue;
+        const uint64_t mh = filters[h]->m;
+        std::vector<int> mem{h};
+        for (size_t b = a + 1; b < cand.size() && mem.size() < (size_t)kMaxStack; b++)
+            if (!done[cand[b]] && mh % filters[cand[b]]->m == 0) mem.push_back(cand[b]);
+        bool explicit_stack = false;
+        uint64_t g = 0;
+        double alone = 0;
+        for (int j : mem) {
+            explicit_stack |= effective_probe_strategy(filters[j], f0->probe_strategy) ==
+                              BLOOMHIP_PROBE_STACKED;
+            g = std::gcd(g, filters[j]->m);
+            alone += probe_cost_alone(filters[j], n);
+        }
+        PartitionWorkspace ws{};
+        if (!plan_stack(mh, g, (int)mem.size(), ncu, &ws)) continue;
+        if (!explicit_stack && (mem.size() < 2 || n < kProbePartitionMinKeys ||
+                                ws.nbins < (size_t)ncu || alone <= kCostStacked))
+            continue;
+        StackTable st{};
+        st.nf = (int)mem.size();
+        for (int k = 0; k < st.nf; k++) {
+            st.words[k] = filters[mem[k]]->d_words;
+            st.nseg[k] = (uint32_t)(filters[mem[k]]->m / ws.seg_bits);
+            st.row[k] = mem[k];
+        }
+        Workspace *w = workspace_for(f0->device, s);
+        std::lock_guard<std::mutex> wl(w->mu);
+        int rc = partition_buffers(w, n, s, &ws);
+        if (rc) return rc;
+        rc = probe_buffers(w, ws, s);
+        if (rc) return rc;
+        hipError_t e = timed(f0, SLOT_PROBE_STACK, s, [&] {
+            return launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s);
+        });
+        if (e != hipSuccess) return fail_hip(e, "stacked probe launch");
+        for (int j : mem) done[j] = 1;
+    }
+    return BLOOMHIP_OK;
+}
+
 // is_set rows of every filter for keys ks into dout (nf x ceil(n/64)), on s
 // (f0->mu held, clears materialised).
 int probe_rows(bloomhip_filter *f0, const bloomhip_filter *const *filters, int nf,
                const KeySpan &ks, size_t n, uint64_t *dout, hipStream_t s) {
     const size_t nw = (n + 63) / 64;
-    int rc = BLOOMHIP_OK;
-    // Small filters: LDS probe, large ones: partitioned probe, one filter at
-    // a time; the rest: gathers, up to kMaxProbeFilters per launch.
+    // Groups of stacked levels first: one partitioned pass each.
+    std::vector<char> done((size_t)nf, 0);
+    int rc = probe_stacks(f0, filters, nf, ks, n, dout, s, done);
+    if (rc) return rc;
+    // Then, one filter at a time: small filters from LDS, large ones
+    // partitioned; the rest: gathers, up to kMaxProbeFilters per launch.
     std::vector<int> gather_idx;
     for (int j = 0; j < nf; j++) {
+        if (done[j]) continue;
         const int kind = probe_kind(filters[j], f0->probe_strategy, n);
         if (kind == BLOOMHIP_PROBE_GATHER) {
             gather_idx.push_back(j);
@@ -651,10 +754,8 @@ int probe_rows(bloomhip_filter *f0, const bloomhip_filter *const *filters, int n
         PartitionWorkspace ws{};
         rc = partition_workspace(w, filters[j]->m, n, s, &ws);
         if (rc) return rc;
-        HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->res), &w->res_bytes,
-                             ws.ntiles * (size_t)kPartTilePos, s));
-        HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->slots), &w->slots_bytes,
-                             ws.ntiles * 3 * kPartTileKeys * sizeof(uint16_t), s));
+        rc = probe_buffers(w, ws, s);
+        if (rc) return rc;
         hipError_t e = timed(f0, SLOT_PROBE_PART, s, [&] {
             return launch_probe_partitioned(ks, filters[j]->mp, filters[j]->d_words, ws, w->res,
                                             w->slots, dout + (size_t)j * nw, s);
@@ -869,7 +970,7 @@ int bloomhip_set_strategy(bloomhip_filter *f, int strategy) {
 
 int bloomhip_set_probe_strategy(bloomhip_filter *f, int strategy) {
     g_last_error.clear();
-    if (!f || strategy < BLOOMHIP_PROBE_AUTO || strategy > BLOOMHIP_PROBE_LDS)
+    if (!f || strategy < BLOOMHIP_PROBE_AUTO || strategy > BLOOMHIP_PROBE_STACKED)
         return BLOOMHIP_EINVAL;
     std::lock_guard<std::mutex> lk(f->mu);
     f->probe_strategy = strategy;

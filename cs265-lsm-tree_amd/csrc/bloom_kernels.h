@@ -77,6 +77,23 @@ constexpr size_t kProbeGatherMaxBytes = 8u << 20;
 constexpr size_t kProbeLdsMinKeys = 1u << 16;
 constexpr size_t kProbePartitionMinKeys = 1u << 18;
 
+// Stacked probe (BLOOMHIP_PROBE_STACKED): up to kMaxStack filters whose sizes
+// all divide the largest one, m_max, probed in ONE partitioned pass.  For
+// m_j | m_max, x % m_j == (x % m_max) % m_j, so the positions modulo m_max
+// alone place every member's bits: with a segment width w dividing every
+// m_j, bit p (< m_max) of segment b = p / w at offset o = p % w lands in
+// member j's segment b % (m_j / w) at the same offset o.  Pass 2 holds the w-bit
+// segment of every member in LDS and writes one result byte per sorted entry
+// (bit j = member j's bit); the combine ANDs each key's three bytes.
+constexpr int kMaxStack = 8;
+
+struct StackTable {
+    const uint32_t *words[kMaxStack];  // member bitmaps (32-bit word view)
+    uint32_t nseg[kMaxStack];          // m_j / w: member j's segment count
+    int row[kMaxStack];                // output row of member j
+    int nf;
+};
+
 struct PartitionWorkspace {
     uint32_t *pos;         // [ntiles * kPartTilePos] tile-sorted positions
     uint32_t *run_rows;    // [ntiles * (nbins + 1)], pass-1 run starts, tile-major
@@ -88,6 +105,11 @@ struct PartitionWorkspace {
     uint32_t nsub;         // pass-1 sub-segments
     uint32_t seg_bits;     // S = group << sub_shift
 };
+
+// Geometry of a stacked probe (seg_bits = w): false when no w = g << s with
+// w | gcd_m, nf * w bits <= kSegMaxBits and <= kPartMaxBins sub-segments
+// exists.  Prefers the widest w that still gives >= ncu segments.
+bool plan_stack(uint64_t m_max, uint64_t gcd_m, int nf, int ncu, PartitionWorkspace *ws);
 
 // CUs of the current device (cached).
 int device_cu_count();
@@ -122,6 +144,12 @@ hipError_t launch_route(const KeySpan &keys, const RouteTable &t, uint64_t *cand
 // each segment in LDS writing one result byte per sorted entry, then AND each
 // key's three bytes into out[ceil(n/64)].  Workspace: res holds
 // ntiles*kPartTilePos bytes, slots ntiles*3*kPartTileKeys u16.
+// Stacked probe of st.nf members (see StackTable) whose largest has
+// ModParams mp_max; ws from plan_stack, res/slots as for the partitioned
+// probe.  Row st.row[j] of out (nw words per row) gets member j's results.
+hipError_t launch_probe_stacked(const KeySpan &keys, const ModParams &mp_max, const StackTable &st,
+                                const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
+                                uint64_t *out, size_t nw, hipStream_t stream);
 hipError_t launch_probe_partitioned(const KeySpan &keys, const ModParams &mp, const uint32_t *words,
                                     const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
                                     uint64_t *out, hipStream_t stream);

@@ -394,7 +394,6 @@ __global__ void __launch_bounds__(kTransposeBlock) k_runs_transpose(
 // ---------------------------------------------------------------------------
 
 constexpr int kApplyBlock = 1024;
-constexpr int kApplyWaves = kApplyBlock / 64;
 constexpr int kApplyDepth = 4;  // lane-group loads per wave per batch
 
 // Lanes per tile for pass 2, from the average run length L = kPartTilePos /
@@ -410,11 +409,14 @@ inline int apply_lanes_per_tile(size_t nbins) {
     return 32;
 }
 
-// PROBE = false: build (OR every entry into the zeroed LDS image, write the
-// segment).  PROBE = true: the LDS image is the filter's segment; each entry's
+// MODE kApplyBuild: OR every entry into the zeroed LDS image, write the
+// segment.  kApplyProbe: the LDS image is the filter's segment; each entry's
 // bit is written as one result byte at the entry's own index in the sorted
 // tile (res[tile*kPartTilePos + index]), so the result stores follow the runs
-// and coalesce like the loads.
+// like the loads.  kApplyStack: LDS holds segment b % nseg[j] of every stack
+// member j (StackTable), the result byte carries member j's bit at bit j.
+// (Writing the results over the positions instead, 4 B each, made the whole
+// probe slower: the combine then reads 4x the bytes; tools/ubench.py stack.)
 //
 // The walk: G consecutive lanes share one tile and read its run as 16-B
 // vectors, lane j of the group starting at the run's 16-B-aligned start
@@ -428,12 +430,17 @@ inline int apply_lanes_per_tile(size_t nbins) {
 // batches of kApplyDepth load groups; the next batch's run bounds are loaded
 // while the current one is applied, and the rare tile whose run outlasts the
 // first step is finished by a wave-uniform loop.
-// ABLATE (timing builds only): 1 = skip the LDS ORs.  The product launches 0.
-template <bool PROBE, int G, int ABLATE = 0>
-__global__ void __launch_bounds__(kApplyBlock) k_part_apply(
+// ABLATE (timing builds only): 1 = skip the LDS ORs (build), 2 = skip the
+// result stores (probe), 3 = non-temporal position loads.  The product
+// launches 0.
+constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2;
+
+template <int MODE, int G, int ABLATE = 0, int BLOCK = kApplyBlock>
+__global__ void __launch_bounds__(BLOCK) k_part_apply(
     const uint32_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, uint32_t seg_bits, uint64_t m, uint32_t *__restrict__ words, uint64_t nw32,
-    int merge_existing, uint8_t *__restrict__ res) {
+    int merge_existing, uint8_t *__restrict__ res, StackTable st) {
+    constexpr bool PROBE = MODE != kApplyBuild;
     static_assert(G >= 1 && G <= 64 && (64 % G) == 0, "G lanes per tile");
     constexpr int kTPI = 64 / G;                     // tiles per load instruction
     constexpr int kBatchTiles = kTPI * kApplyDepth;  // tiles per wave batch
@@ -451,11 +458,20 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
     const int nseg = (int)(min(nw32, w0 + seg_words) - w0);  // last segment may be short
     const uint32_t base = (uint32_t)b * seg_bits;             // entries are full positions
     const uint32_t lim = (uint32_t)min((uint64_t)seg_bits, m - base);
-    if constexpr (PROBE) {
-        for (int i = threadIdx.x; i < (int)seg_words; i += kApplyBlock)
+    if constexpr (MODE == kApplyStack) {
+        // member j's segment b % nseg[j]: seg_words is a multiple of 4 and
+        // every member is a whole number of segments (plan_stack)
+        for (int j = 0; j < st.nf; j++) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(
+                st.words[j] + (size_t)((uint32_t)b % st.nseg[j]) * seg_words);
+            uint4 *dst = reinterpret_cast<uint4 *>(seg + (size_t)j * seg_words);
+            for (int i = threadIdx.x; i < (int)seg_words / 4; i += BLOCK) dst[i] = src[i];
+        }
+    } else if constexpr (MODE == kApplyProbe) {
+        for (int i = threadIdx.x; i < (int)seg_words; i += BLOCK)
             seg[i] = i < nseg ? words[w0 + i] : 0u;
     } else {
-        for (int i = threadIdx.x; i < (int)seg_words / 4; i += kApplyBlock)
+        for (int i = threadIdx.x; i < (int)seg_words / 4; i += BLOCK)
             reinterpret_cast<uint4 *>(seg)[i] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
@@ -479,6 +495,12 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
         }
     };
     auto load = [&](int t, uint32_t e) -> uint4 {
+        if constexpr (ABLATE == 3) {
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            const v4u x = __builtin_nontemporal_load(
+                reinterpret_cast<const v4u *>(pos + (size_t)t * kPartTilePos + e));
+            return make_uint4(x[0], x[1], x[2], x[3]);
+        }
         return *reinterpret_cast<const uint4 *>(pos + (size_t)t * kPartTilePos + e);
     };
     auto apply1 = [&](uint32_t v, int t, uint32_t e) {
@@ -487,7 +509,7 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
             asm volatile("" ::"v"(o));
             (void)t; (void)e;
         } else if (o < lim) {
-            if constexpr (PROBE) {
+            if constexpr (PROBE) {  // (ABLATE builds only; apply4 handles probes)
                 res[(size_t)t * kPartTilePos + e] = (seg[o >> 5] >> (o & 31)) & 1u;
             } else {
                 (void)t; (void)e;
@@ -496,23 +518,50 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
         }
     };
     auto apply4 = [&](const uint4 &v, int t, uint32_t e) {
-        if constexpr (PROBE && ABLATE == 0) {
+        if constexpr (PROBE && ABLATE != 1) {
             // the 4 result bytes go out as one dword when all 4 entries are
             // this segment's (inside a run), else byte by byte
-            // LDS reads unconditional (word 0 for other segments' entries),
-            // so the four issue back to back under one wait
+            // LDS reads unconditional (offset 0 for other segments' entries),
+            // so they issue back to back under one wait
             const uint32_t o[4] = {v.x - base, v.y - base, v.z - base, v.w - base};
-            uint32_t w[4], bits = 0, mask = 0;
+            uint32_t bits = 0, mask = 0;
+            if constexpr (MODE == kApplyStack) {
+                uint32_t oo[4], r[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-            for (int k = 0; k < 4; k++) w[k] = seg[o[k] < lim ? o[k] >> 5 : 0u];
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t ok = o[k] < lim ? 1u : 0u;
+                    mask |= ok << k;
+                    oo[k] = ok ? o[k] : 0u;
+                }
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t ok = o[k] < lim ? 1u : 0u;
-                mask |= ok << k;
-                bits |= (((w[k] >> (o[k] & 31)) & ok) << (8 * k));
+                for (int j = 0; j < kMaxStack; j++) {
+                    if (j < st.nf) {
+                        const uint32_t *img = seg + (size_t)j * seg_words;
+                        uint32_t w[4];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) w[k] = img[oo[k] >> 5];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) r[k] |= ((w[k] >> (oo[k] & 31)) & 1u) << j;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) bits |= (mask >> k & 1u) ? r[k] << (8 * k) : 0u;
+            } else {
+                uint32_t w[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) w[k] = seg[o[k] < lim ? o[k] >> 5 : 0u];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t ok = o[k] < lim ? 1u : 0u;
+                    mask |= ok << k;
+                    bits |= (((w[k] >> (o[k] & 31)) & ok) << (8 * k));
+                }
             }
             uint8_t *p = res + (size_t)t * kPartTilePos + e;
-            if (mask == 0xFu) {
+            if constexpr (ABLATE == 2) {
+                asm volatile("" ::"v"(bits), "v"(mask));
+                (void)p;
+            } else if (mask == 0xFu) {
                 *reinterpret_cast<uint32_t *>(p) = bits;
             } else if (mask != 0) {
 #pragma unroll
@@ -529,7 +578,7 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
 
     uint2 r[kApplyDepth];
     if (wave < nbatch) bounds(wave, r);
-    for (int j = wave; j < nbatch; j += kApplyWaves) {
+    for (int j = wave; j < nbatch; j += (BLOCK / 64)) {
         int t[kApplyDepth];
         uint32_t e[kApplyDepth];
         uint4 v[kApplyDepth];
@@ -540,7 +589,7 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
             v[d] = load(t[d], min(e[d], kLastVec));
         }
         uint2 rn[kApplyDepth];
-        const int jn = j + kApplyWaves;
+        const int jn = j + (BLOCK / 64);
         if (jn < nbatch) bounds(jn, rn);
 #pragma unroll
         for (int d = 0; d < kApplyDepth; d++) apply4(v[d], t[d], min(e[d], kLastVec));
@@ -561,7 +610,7 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
     if (nseg == (int)seg_words) {  // seg_words % 4 == 0 and w0 is 16-B aligned
         uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
         const uint4 *seg4 = reinterpret_cast<const uint4 *>(seg);
-        for (int q = threadIdx.x; q < (int)seg_words / 4; q += kApplyBlock) {
+        for (int q = threadIdx.x; q < (int)seg_words / 4; q += BLOCK) {
             uint4 v = seg4[q];
             if (merge_existing) {
                 const uint4 o = dst4[q];
@@ -570,7 +619,7 @@ __global__ void __launch_bounds__(kApplyBlock) k_part_apply(
             dst4[q] = v;
         }
     } else {
-        for (int i = threadIdx.x; i < nseg; i += kApplyBlock) {
+        for (int i = threadIdx.x; i < nseg; i += BLOCK) {
             uint32_t v = seg[i];
             if (merge_existing) v |= dst[i];
             dst[i] = v;
@@ -671,14 +720,15 @@ __global__ void __launch_bounds__(kProbeLdsBlock) k_probe_lds(KeySpan ks, const 
     }
 }
 
-// Partitioned probe, last step (k_probe_combine): one workgroup per tile
-// stages the tile's result bytes (sorted order) in LDS and, for each key,
-// ANDs the bytes at its three slots; a 64-lane ballot packs 64 keys per u64.
+// Partitioned / stacked probe, last step (k_probe_combine): one workgroup per
+// tile stages the tile's result bytes (sorted order) in LDS and, for each key,
+// ANDs the bytes at its three slots; bit j of the AND is filter j's is_set,
+// packed 64 keys per u64 by a 64-lane ballot into row rows.row[j] of out.
 constexpr int kCombineBlock = 256;
 
 __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, size_t n,
-    uint64_t *__restrict__ out) {
+    uint64_t *__restrict__ out, size_t nw, StackTable rows) {
     __shared__ __attribute__((aligned(16))) uint8_t s_r[kPartTilePos];
     const size_t tile = blockIdx.x;
     const size_t tile0 = tile * kPartTileKeys;
@@ -691,12 +741,14 @@ __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int j = 0; j < (int)kPartTileKeys / kCombineBlock; j++) {
         const int key = j * kCombineBlock + (int)threadIdx.x;
-        bool hit = false;
+        uint32_t hit = 0;
         if (key < tile_keys)
             hit = s_r[sl[key]] & s_r[sl[kPartTileKeys + key]] & s_r[sl[2 * kPartTileKeys + key]];
-        const uint64_t ballot = __ballot(hit);
         const int base = j * kCombineBlock + wave * 64;
-        if (lane == 0 && base < tile_keys) out[(tile0 + base) / 64] = ballot;
+        for (int f = 0; f < rows.nf; f++) {
+            const uint64_t ballot = __ballot((hit >> f) & 1u);
+            if (lane == 0 && base < tile_keys) out[(size_t)rows.row[f] * nw + (tile0 + base) / 64] = ballot;
+        }
     }
 }
 
@@ -898,6 +950,46 @@ bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
     return true;
 }
 
+bool plan_stack(uint64_t m_max, uint64_t gcd_m, int nf, int ncu, PartitionWorkspace *ws) {
+    if (m_max == 0 || m_max > 0xFFFFFFFFull || nf < 1 || nf > kMaxStack || gcd_m == 0 ||
+        m_max % gcd_m != 0)
+        return false;
+    const uint64_t wmax = kSegMaxBits / (uint64_t)nf;  // every member's w bits in LDS
+    uint32_t s0 = 5;
+    while ((((m_max - 1) >> s0) + 1) > kPartMaxBins) s0++;
+    // candidates w = g << s dividing gcd_m (so every member, and m_max, is a
+    // whole number of segments), 128-bit multiples for the 16-B image loads
+    uint64_t best_w = 0;
+    uint32_t best_s = 0;
+    // The segment count sets the run length per tile (kPartTilePos / nbins),
+    // w only the LDS image: the widest w that still gives every CU a segment,
+    // else (small m_max) the narrowest, for the most segments.
+    auto better = [&](uint64_t w) {
+        if (best_w == 0) return true;
+        const bool a = m_max / w >= (uint64_t)ncu, b = m_max / best_w >= (uint64_t)ncu;
+        if (a != b) return a;
+        return a ? w > best_w : w < best_w;
+    };
+    for (uint32_t s = s0; s < 32 && (1ull << s) <= wmax; s++) {
+        if (gcd_m % (1ull << s)) break;  // larger s cannot divide either
+        for (uint64_t g = wmax >> s; g >= 1; g--) {
+            const uint64_t w = g << s;
+            if (w % 128 || gcd_m % w) continue;
+            if (better(w) || (w == best_w && s > best_s)) {
+                best_w = w;
+                best_s = s;
+            }
+        }
+    }
+    if (best_w == 0) return false;
+    ws->sub_shift = best_s;
+    ws->group = (uint32_t)(best_w >> best_s);
+    ws->nsub = (uint32_t)(m_max >> best_s);
+    ws->seg_bits = (uint32_t)best_w;
+    ws->nbins = (size_t)(m_max / best_w);
+    return true;
+}
+
 hipError_t launch_runs_transpose(const PartitionWorkspace &ws, hipStream_t stream) {
     const int width = (int)ws.nbins + 1;
     const dim3 grid((unsigned)((width + kTransposeTile - 1) / kTransposeTile),
@@ -943,32 +1035,35 @@ hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const Partiti
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
-template <bool PROBE, int G>
+template <int MODE, int G>
 hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
-                          uint64_t nw32, int merge, uint8_t *res, hipStream_t stream) {
+                          uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
+                          hipStream_t stream) {
     static const bool attr_set = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<PROBE, G>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<MODE, G>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kSegMaxBits / 8));
         return true;
     }();
     (void)attr_set;
-    k_part_apply<PROBE, G><<<(unsigned)ws.nbins, kApplyBlock, ws.seg_bits / 8, stream>>>(
+    const size_t lds = (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
+    if (lds > kSegMaxBits / 8) return hipErrorInvalidValue;
+    k_part_apply<MODE, G><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
-        res);
+        res, st);
     return hipGetLastError();
 }
 
-template <bool PROBE>
+template <int MODE>
 hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *words, uint64_t nw32,
-                        int merge, uint8_t *res, hipStream_t stream) {
+                        int merge, uint8_t *res, const StackTable &st, hipStream_t stream) {
     switch (apply_lanes_per_tile(ws.nbins)) {
-        case 2: return launch_apply_g<PROBE, 2>(ws, m, words, nw32, merge, res, stream);
-        case 4: return launch_apply_g<PROBE, 4>(ws, m, words, nw32, merge, res, stream);
-        case 8: return launch_apply_g<PROBE, 8>(ws, m, words, nw32, merge, res, stream);
-        case 16: return launch_apply_g<PROBE, 16>(ws, m, words, nw32, merge, res, stream);
-        case 32: return launch_apply_g<PROBE, 32>(ws, m, words, nw32, merge, res, stream);
-        default: return launch_apply_g<PROBE, 64>(ws, m, words, nw32, merge, res, stream);
+        case 2: return launch_apply_g<MODE, 2>(ws, m, words, nw32, merge, res, st, stream);
+        case 4: return launch_apply_g<MODE, 4>(ws, m, words, nw32, merge, res, st, stream);
+        case 8: return launch_apply_g<MODE, 8>(ws, m, words, nw32, merge, res, st, stream);
+        case 16: return launch_apply_g<MODE, 16>(ws, m, words, nw32, merge, res, st, stream);
+        case 32: return launch_apply_g<MODE, 32>(ws, m, words, nw32, merge, res, st, stream);
+        default: return launch_apply_g<MODE, 64>(ws, m, words, nw32, merge, res, st, stream);
     }
 }
 
@@ -976,7 +1071,8 @@ hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const Partiti
                              int merge_existing, hipStream_t stream) {
     if (ws.ntiles == 0) return hipSuccess;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
-    return launch_apply<false>(ws, mp.m, words, nw32, merge_existing, nullptr, stream);
+    return launch_apply<kApplyBuild>(ws, mp.m, words, nw32, merge_existing, nullptr, StackTable{},
+                                     stream);
 }
 
 hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, const uint32_t *words,
@@ -987,9 +1083,30 @@ hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, cons
     if (e != hipSuccess) return e;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
     uint32_t *w = const_cast<uint32_t *>(words);  // read-only in PROBE mode
-    e = launch_apply<true>(ws, mp.m, w, nw32, 0, res, stream);
+    e = launch_apply<kApplyProbe>(ws, mp.m, w, nw32, 0, res, StackTable{}, stream);
     if (e != hipSuccess) return e;
-    k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out);
+    StackTable rows{};
+    rows.nf = 1;
+    k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out,
+                                                                       (ks.n + 63) / 64, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, const StackTable &st,
+                                const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
+                                uint64_t *out, size_t nw, hipStream_t stream) {
+    if (ks.n == 0) return hipSuccess;
+    if (st.nf < 1 || st.nf > kMaxStack || !mp_max.fast || ws.seg_bits % 128 != 0 ||
+        (uint64_t)ws.nbins * ws.seg_bits != mp_max.m)
+        return hipErrorInvalidValue;
+    for (int j = 0; j < st.nf; j++)
+        if (st.nseg[j] == 0 || ws.nbins % st.nseg[j] != 0) return hipErrorInvalidValue;
+    hipError_t e = launch_bin<true>(ks, mp_max, ws, slots, stream);
+    if (e != hipSuccess) return e;
+    e = launch_apply<kApplyStack>(ws, mp_max.m, nullptr, 0, 0, res, st, stream);
+    if (e != hipSuccess) return e;
+    k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out, nw,
+                                                                       st);
     return hipGetLastError();
 }
 

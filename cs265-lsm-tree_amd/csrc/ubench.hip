@@ -157,11 +157,11 @@ extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_
     if (variant == 0) variant = apply_lanes_per_tile(ws.nbins);
 #define UB_APPLY(G, A)                                                                        \
     do {                                                                                      \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<false, G, A>), \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<kApplyBuild, G, A>), \
                                   hipFuncAttributeMaxDynamicSharedMemorySize,                 \
                                   (int)(kSegMaxBits / 8));                                    \
-        k_part_apply<false, G, A><<<nbins, kApplyBlock, sb / 8, s>>>(                         \
-            pos, run_starts, ntiles, nbins, sb, m, words, nw32, 0, nullptr);                  \
+        k_part_apply<kApplyBuild, G, A><<<nbins, kApplyBlock, sb / 8, s>>>(                         \
+            pos, run_starts, ntiles, nbins, sb, m, words, nw32, 0, nullptr, StackTable{});    \
     } while (0)
     switch (variant) {
         case 2: UB_APPLY(2, 0); break;
@@ -178,5 +178,102 @@ extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_
         default: return -22;
     }
 #undef UB_APPLY
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// The stacked probe (C3 by default) by phase: 0 = the product's three
+// launches, 1 = pass 1 (with slots), 2 = pass 2 alone (G from
+// apply_lanes_per_tile), 3 = pass 2 without its result stores, 4 = pass 2
+// reading only member 0's image, 5 = the combine; 100 + G = pass 2 with G
+// lanes per tile.  Buffers sized by the caller for plan_stack's geometry
+// (ubench_stack_geometry; runs: both layouts).  Members must divide the
+// largest, so their gcd is the smallest.
+namespace {
+bool ub_stack_plan(int nf, const uint64_t *ms, uint64_t *mmax, PartitionWorkspace *ws) {
+    uint64_t g = 0;
+    *mmax = 0;
+    for (int j = 0; j < nf; j++) {
+        *mmax = ms[j] > *mmax ? ms[j] : *mmax;
+        g = g == 0 || ms[j] < g ? ms[j] : g;
+    }
+    return plan_stack(*mmax, g, nf, device_cu_count(), ws);
+}
+}  // namespace
+
+extern "C" int ubench_stack_geometry(int nf, const uint64_t *ms, uint64_t *nbins_out,
+                                     uint64_t *seg_bits_out) {
+    uint64_t mmax = 0;
+    PartitionWorkspace ws{};
+    if (!ub_stack_plan(nf, ms, &mmax, &ws)) return -34;
+    *nbins_out = ws.nbins;
+    *seg_bits_out = ws.seg_bits;
+    return 0;
+}
+
+extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, const uint64_t *ms,
+                            void *const *words, uint32_t *pos, uint32_t *runs, uint8_t *res,
+                            uint16_t *slots, uint64_t *out, void *stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
+    uint64_t mmax = 0;
+    PartitionWorkspace ws{};
+    if (!ub_stack_plan(nf, ms, &mmax, &ws)) return -34;
+    ws.ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
+    ws.pos = pos;
+    ws.run_rows = runs;
+    ws.run_starts = runs + ws.ntiles * (ws.nbins + 1);
+    StackTable st{};
+    st.nf = nf;
+    for (int j = 0; j < nf; j++) {
+        st.words[j] = reinterpret_cast<const uint32_t *>(words[j]);
+        st.nseg[j] = (uint32_t)(ms[j] / ws.seg_bits);
+        st.row[j] = j;
+    }
+    const ModParams mp = make_mod_params(mmax);
+    const size_t nw = (n + 63) / 64;
+    const size_t lds = (size_t)ws.seg_bits / 8 * nf;
+#define UB_STACK(G, A, T) UB_STACKB(G, A, T, kApplyBlock)
+#define UB_STACKB(G, A, T, B)                                                                      \
+    do {                                                                                           \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<kApplyStack, G, A, B>), \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,                      \
+                                  (int)(kSegMaxBits / 8));                                         \
+        k_part_apply<kApplyStack, G, A, B><<<(unsigned)ws.nbins, B, lds, s>>>(                     \
+            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, mmax, nullptr, 0,   \
+            0, res, T);                                                                            \
+    } while (0)
+    const int G = apply_lanes_per_tile(ws.nbins);
+    StackTable one = st;
+    one.nf = 1;
+    switch (variant) {
+        case 0: return launch_probe_stacked(ks, mp, st, ws, res, slots, out, nw, s) == hipSuccess ? 0 : -5;
+        case 1: return launch_bin<true>(ks, mp, ws, slots, s) == hipSuccess ? 0 : -5;
+        case 2: return launch_apply<kApplyStack>(ws, mmax, nullptr, 0, 0, res, st, s) == hipSuccess ? 0 : -5;
+        case 3:
+            if (G == 4) UB_STACK(4, 2, st); else if (G == 8) UB_STACK(8, 2, st); else return -22;
+            break;
+        case 4:
+            if (G == 4) UB_STACK(4, 0, one); else if (G == 8) UB_STACK(8, 0, one); else return -22;
+            break;
+        case 5:
+            k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, s>>>(res, slots, n, out, nw, st);
+            break;
+        case 6:
+            if (G == 4) UB_STACK(4, 3, st); else if (G == 8) UB_STACK(8, 3, st); else return -22;
+            break;
+        case 8:
+            if (G == 4) UB_STACKB(4, 0, st, 512); else if (G == 8) UB_STACKB(8, 0, st, 512); else return -22;
+            break;
+        case 10:
+            if (G == 4) UB_STACKB(4, 2, st, 512); else if (G == 8) UB_STACKB(8, 2, st, 512); else return -22;
+            break;
+        case 102: UB_STACK(2, 0, st); break;
+        case 104: UB_STACK(4, 0, st); break;
+        case 108: UB_STACK(8, 0, st); break;
+        case 116: UB_STACK(16, 0, st); break;
+        default: return -22;
+    }
+#undef UB_STACK
+#undef UB_STACKB
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -66,6 +66,11 @@ extern "C" {
 #define BLOOMHIP_PROBE_GATHER 1    /* per-key gathers of the 3 bits */
 #define BLOOMHIP_PROBE_PARTITION 2 /* bin positions by segment, test in LDS */
 #define BLOOMHIP_PROBE_LDS 3       /* whole filter staged in each workgroup's LDS (m/8 <= 160 KiB) */
+/* One partitioned pass for up to 8 filters whose sizes all divide the largest
+ * one's (x % m_j == (x % m_max) % m_j): an LSM's stacked levels, where run
+ * capacities grow by the fanout (src/lsm_tree.cpp:36-41).  AUTO picks it for
+ * such groups when it beats probing the members one by one. */
+#define BLOOMHIP_PROBE_STACKED 4
 
 typedef struct bloomhip_filter bloomhip_filter;
 
@@ -211,7 +216,7 @@ int bloomhip_resolve_strategy(const bloomhip_filter *f, size_t n, int *strategy_
  * is bracketed by HIP events on its stream; bloomhip_profile_read returns,
  * for kernel slot `slot` (0..BLOOMHIP_PROF_SLOTS-1), its name, launch count
  * and summed device milliseconds (it synchronises the stream). */
-#define BLOOMHIP_PROF_SLOTS 9
+#define BLOOMHIP_PROF_SLOTS 10
 int bloomhip_profile_enable(bloomhip_filter *f, int enable);
 int bloomhip_profile_read(bloomhip_filter *f, int slot, const char **name_out,
                           uint64_t *launches_out, double *ms_out);

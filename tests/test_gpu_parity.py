@@ -195,12 +195,12 @@ def test_deferred_clear_then_build_and_probe(coracle, strategy):
 
 
 # ---------------------------------------------------------------- probe ----
-PROBES = [bh.PROBE_GATHER, bh.PROBE_PARTITION, bh.PROBE_LDS]
-PROBE_IDS = ["gather", "partition", "lds"]
+PROBES = [bh.PROBE_GATHER, bh.PROBE_PARTITION, bh.PROBE_LDS, bh.PROBE_STACKED]
+PROBE_IDS = ["gather", "partition", "lds", "stacked"]
 
 
 @pytest.mark.parametrize("m", [1, 64, 65, 1000, 655_360, 1_000_003, 167_772_160, 671_088_640,
-                               2**32 - 1, 2**32 + 15])
+                               0xFFFFFF00, 2**32 - 1, 2**32 + 15])
 @pytest.mark.parametrize("probe", PROBES, ids=PROBE_IDS)
 def test_probe_matches_oracle(coracle, m, probe):
     keys = rand_keys(100_000 if m < 2**32 else 20_000, 21)
@@ -253,6 +253,64 @@ def test_probe_device_buffers_and_strides(coracle, torch_cuda, probe):
     aos[:, 0] = keys
     got = bh.test_batch([f], aos.reshape(-1), n=keys.size, stride=8)[0]
     assert (got == ref).all()
+
+
+def _stack_case(coracle, ms, probe_keys, strategies=None, stride=4, seed=0):
+    filters, refs = [], []
+    for j, m in enumerate(ms):
+        keys = rand_keys(int(min(40_000, max(64, m // 10))), 500 + seed + j)
+        f = bh.BloomFilter(m)
+        f.set_probe_strategy(strategies[j] if strategies else bh.PROBE_STACKED)
+        f.set_batch(keys)
+        filters.append(f)
+        refs.append((m, coracle.build(m, keys)))
+        probe_keys[j * 1000:(j + 1) * 1000] = keys[:1000]   # some hits per filter
+    if stride == 8:
+        aos = np.zeros((probe_keys.size, 2), dtype=np.int32)
+        aos[:, 0] = probe_keys
+        got = bh.test_batch(filters, aos.reshape(-1), n=probe_keys.size, stride=8)
+    else:
+        got = bh.test_batch(filters, probe_keys)
+    for j, (m, w) in enumerate(refs):
+        assert (got[j] == coracle.test(w, m, probe_keys)).all(), (j, m)
+
+
+@pytest.mark.parametrize("ms", [
+    [10_240 * 4**i for i in range(5)],            # C3's level geometry, scaled down 64x
+    [655_360 * 4**i for i in range(4)],           # C3 levels 0-3
+    [2**22, 2**20, 2**22, 2**16],                 # powers of two, a repeated size
+    [1_000_000, 1_000_000],                       # no 128-bit-multiple w divides 10^6
+    [3 * 2**20, 2**20, 3 * 2**18, 2**18, 2**19, 3 * 2**17, 2**17, 2**16, 2**15],  # 9 members
+    [5 * 2**21, 2**21, 1_000_003, 5 * 2**19, 2**32 + 15],  # non-divisors, > 2^32 mixed in
+], ids=["c3x64", "c3_l0-3", "pow2", "no_w", "nine", "mixed"])
+def test_stacked_probe_matches_oracle(coracle, ms):
+    probe = rand_keys(300_001, 77)
+    _stack_case(coracle, ms, probe)
+
+
+def test_stacked_probe_auto_and_strided(coracle):
+    """AUTO stacks a divisible group at >= 2^18 keys; AoS entry_t keys."""
+    ms = [655_360 * 4**i for i in range(5)]
+    probe = rand_keys(270_000, 78)
+    _stack_case(coracle, ms, probe, strategies=[bh.PROBE_AUTO] * 5)
+    _stack_case(coracle, ms[:3], rand_keys(263_001, 79), stride=8, seed=7)
+
+
+def test_stacked_probe_profile_slot():
+    """The stacked pass runs (and is timed) when AUTO should pick it."""
+    ms = [655_360 * 4**i for i in range(5)]
+    filters = []
+    for j, m in enumerate(ms):
+        f = bh.BloomFilter(m)
+        f.set_batch(rand_keys(10_000, j))
+        filters.append(f)
+    f0 = filters[0]
+    f0.profile(True)
+    f0.profile_reset()
+    bh.test_batch(filters, rand_keys(1 << 19, 5))
+    prof = f0.profile_read()
+    f0.profile(False)
+    assert prof.get("probe_stacked", {}).get("launches") == 1, prof
 
 
 def test_probe_empty():

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""C3 probe (16.8M GETs x 5 level filters) repeated under one strategy, for
+rocprofv3 --kernel-trace --stats: `python tools/probe_prof.py [auto|stacked|
+partition|gather] [reps]`."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
+import bloomhip as bh  # noqa: E402
+from bloomhip import workloads as W  # noqa: E402
+
+
+def main():
+    kind = sys.argv[1] if len(sys.argv) > 1 else "auto"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    st = {"auto": bh.PROBE_AUTO, "stacked": bh.PROBE_STACKED, "partition": bh.PROBE_PARTITION,
+          "gather": bh.PROBE_GATHER}[kind]
+    torch.cuda.set_device(0)
+    gets, levels = W.c3()
+    dgets = torch.from_numpy(gets).cuda()
+    filters = []
+    for lvl, keys, m in levels:
+        f = bh.BloomFilter(m)
+        f.set_batch(keys)
+        f.set_probe_strategy(st)
+        filters.append(f)
+    out = torch.empty((len(filters), (gets.size + 63) // 64), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream()
+    for _ in range(reps):
+        bh.test_batch(filters, dgets, out=out, stream=s)
+    torch.cuda.synchronize()
+    print("done", kind, reps)
+
+
+if __name__ == "__main__":
+    main()

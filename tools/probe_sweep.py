@@ -61,6 +61,25 @@ def main():
     for nf in (3, 4, 5):
         ms = timed(lambda s: bh.test_batch(filters[:nf], dgets, out=out[:nf], stream=s))
         print(json.dumps({"levels": nf, "auto_us": round(ms * 1e3, 1)}), flush=True)
+    # Stacked pass vs the members probed one by one (their own best kind).
+    alone = [bh.PROBE_LDS, bh.PROBE_GATHER, bh.PROBE_GATHER, bh.PROBE_GATHER, bh.PROBE_PARTITION]
+    for sub in ([0, 1, 2, 3, 4], [0, 1, 2, 3], [1, 2, 3], [3, 4], [0, 4], [2, 3]):
+        fs = [filters[i] for i in sub]
+        o = out[:len(sub)]
+        for i in sub:
+            filters[i].set_probe_strategy(bh.PROBE_STACKED)
+        st_us = timed(lambda s: bh.test_batch(fs, dgets, out=o, stream=s)) * 1e3
+        got = o.cpu().clone()
+        for i in sub:
+            filters[i].set_probe_strategy(alone[i])
+        al_us = timed(lambda s: bh.test_batch(fs, dgets, out=o, stream=s)) * 1e3
+        assert torch.equal(got, o.cpu()), f"stacked {sub} disagrees"
+        for i in sub:
+            filters[i].set_probe_strategy(bh.PROBE_AUTO)
+        au_us = timed(lambda s: bh.test_batch(fs, dgets, out=o, stream=s)) * 1e3
+        print(json.dumps({"levels": sub, "stacked_us": round(st_us, 1),
+                          "one_by_one_us": round(al_us, 1), "auto_us": round(au_us, 1)}),
+              flush=True)
     for st_name, st in (("all gather", bh.PROBE_GATHER),):
         for f in filters:
             f.set_probe_strategy(st)

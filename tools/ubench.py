@@ -21,6 +21,12 @@ LIB.ubench_part_bin.restype = ctypes.c_int
 LIB.ubench_part_apply.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
 LIB.ubench_part_apply.restype = ctypes.c_int
+LIB.ubench_stack.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                             ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_void_p] * 6
+LIB.ubench_stack.restype = ctypes.c_int
+LIB.ubench_stack_geometry.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p]
+LIB.ubench_stack_geometry.restype = ctypes.c_int
 
 
 def timeit(which, buf, nbytes, m, grid, block, iters, reps=5):
@@ -151,8 +157,66 @@ def overlap(n=16_777_216, bpe=10.0):
                           "us": round(a.elapsed_time(b) / 20 * 1e3, 2)}), flush=True)
 
 
+def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
+    """The stacked C3 probe by phase (ubench_stack variants), and pass 2 with
+    its result stores or 4 of its 5 member reads removed."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
+    import bloomhip as bh
+    from bloomhip import workloads as W
+    gets, levels = W.c3()
+    filters, ms = [], []
+    for lvl, keys, m in levels:
+        if lvl in levels_sel:
+            f = bh.BloomFilter(m)
+            f.set_batch(keys)
+            filters.append(f)
+            ms.append(m)
+    nf = len(ms)
+    msa = np.array(ms, dtype=np.uint64)
+    wp = (ctypes.c_void_p * nf)(*[f.device_words_ptr() for f in filters])
+    nb, sb = ctypes.c_uint64(), ctypes.c_uint64()
+    assert LIB.ubench_stack_geometry(nf, msa.ctypes.data, ctypes.byref(nb), ctypes.byref(sb)) == 0
+    n = gets.size
+    ntiles = (n + 4095) // 4096
+    dk = torch.from_numpy(gets).cuda()
+    pos = torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda")
+    runs = torch.empty(2 * ntiles * (nb.value + 1), dtype=torch.int32, device="cuda")
+    res = torch.empty(ntiles * 12288, dtype=torch.uint8, device="cuda")
+    slots = torch.empty(ntiles * 12288, dtype=torch.int16, device="cuda")
+    out = torch.empty(nf * ((n + 63) // 64), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream()
+
+    def run(v):
+        return LIB.ubench_stack(v, dk.data_ptr(), n, nf, msa.ctypes.data, wp, pos.data_ptr(),
+                                runs.data_ptr(), res.data_ptr(), slots.data_ptr(), out.data_ptr(),
+                                s.cuda_stream)
+    assert run(0) == 0
+    names = {0: "all three", 1: "pass 1 (+slots, +transpose)", 2: "pass 2",
+             3: "pass 2, no result stores", 4: "pass 2, member 0 image only", 5: "combine",
+             6: "pass 2, non-temporal position loads",
+             102: "pass 2 G=2", 104: "pass 2 G=4", 108: "pass 2 G=8", 116: "pass 2 G=16",
+             8: "pass 2, 512-thread blocks", 10: "pass 2, 512-thread blocks, no result stores"}
+    for v in names:
+        if run(v) != 0:
+            continue
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(20):
+            run(v)
+        b.record(s)
+        torch.cuda.synchronize()
+        print(json.dumps({"op": "stacked probe", "levels": list(levels_sel), "nbins": nb.value,
+                          "seg_bits": sb.value, "phase": names[v],
+                          "us": round(a.elapsed_time(b) / 20 * 1e3, 1)}), flush=True)
+
+
 def main():
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "stack":
+        stack_ablation()
+        return stack_ablation((0, 1, 2, 3))
     if len(sys.argv) > 1 and sys.argv[1] == "isa":
         return isa_rates()
     if len(sys.argv) > 1 and sys.argv[1] == "part":
