@@ -143,6 +143,31 @@ def route_c3(torch, bh, steps, warmup):
             "keys_with_candidate": routed}
 
 
+def compact_fanin(torch, bh, reps):
+    """§8f row 3: a fan-in-4 compaction (4 runs x 4M entries, newest first)
+    merged on the device and fused with the new run's filter + fence build
+    (bloomhip_compact, synchronous), device-resident in and out."""
+    from bloomhip import workloads as W
+    runs, m = W.compaction_fanin()
+    druns = [torch.from_numpy(r).cuda() for r in runs]
+    total = sum(r.shape[0] for r in runs)
+    dout = torch.empty((total, 2), dtype=torch.int32, device="cuda")
+    f = bh.BloomFilter(m)
+    for _ in range(2):
+        got = bh.compact(druns, drop_tombstones=True, filter=f, out=dout)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        f.clear()
+        got = bh.compact(druns, drop_tombstones=True, filter=f, out=dout)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    return {"gentries_s": round(total / t / 1e9, 3), "ms": round(t * 1e3, 3),
+            "entries_in": total, "entries_out": int(got.shape[0]),
+            "note": "4 sorted runs merged newest-wins + tombstones dropped + filter/fences "
+                    "of the merged run built; wall clock per synchronous call"}
+
+
 def e2e_build(torch, bh, keys_np, m, reps=5):
     """Host keys (pinned) -> device -> filter -> host bitmap, wall clock."""
     import numpy as np
@@ -279,6 +304,8 @@ def main():
         extras["probe_c3"] = probe_c3(torch, bh, max(5, args.steps // 5), 2)
         log("route C3 ...")
         extras["route_c3"] = route_c3(torch, bh, max(5, args.steps // 5), 2)
+        log("compact ...")
+        extras["compact_fanin4"] = compact_fanin(torch, bh, max(3, args.steps // 20))
         log("e2e ...")
         extras["e2e_build"] = e2e_build(torch, bh, keys, m)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

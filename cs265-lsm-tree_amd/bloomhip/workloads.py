@@ -87,6 +87,22 @@ def c3_runs(seed: int = SEED):
     return gets, [(lvl, np.unique(keys), m) for lvl, keys, m in levels]
 
 
+def compaction_fanin(seed: int = SEED, fanout: int = 4, cap: int = C2_N // 4):
+    """A level's compaction fan-in (LSMTree::merge_down, src/lsm_tree.cpp:48-95):
+    `fanout` runs of `cap` entries each (generator --puts streams, seeds seed+j,
+    each run its distinct keys ascending with their last-written values, as a
+    flush writes it), newest first, merged into one run whose filter is sized
+    for fanout * cap entries at 10 bits/key (C2's m for the defaults)."""
+    runs = []
+    for j in range(fanout):
+        keys, vals = gen_puts(seed + j, cap, with_vals=True)
+        # the newest value of a repeated key: last occurrence in the stream
+        rk, rv = keys[::-1], vals[::-1]
+        uk, first = np.unique(rk, return_index=True)
+        runs.append(np.ascontiguousarray(np.stack([uk, rv[first]], axis=1)))
+    return runs, m_bits(fanout * cap, C2_BPE)
+
+
 def c4(seed: int = SEED, n: int = C4_N):
     return gen_puts(seed, n), m_bits(n, C4_BPE)
 

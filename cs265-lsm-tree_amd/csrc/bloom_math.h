@@ -25,20 +25,41 @@ namespace bloomhip {
 #define BH_HD __host__ __device__ __forceinline__
 
 // ---- the three reference hashes, before the modulo --------------------------
+// Each chain is the reference's, rewritten only where an identity on the
+// sign-extended key saves gfx950 instructions (same value mod 2^64):
+//   ~x + (x << 15)            == x * 32767 - 1        (one v_mad_i64_i32 on the
+//   (x + c) + (x << 12)       == x * 4097 + c          int32 key)
+//   x + (x << s)              == lshl_add(x, s, x)    (one v_lshl_add_u64; the
+//   x * 2057                  == (x << 11) + lshl_add(x, 3, x)   (the compiler
+//                                                          emits a 64-bit multiply)
+// tests/test_host.py fuzzes the host build of these against the oracle.
+
+// (a << S) + b in 64 bits.  v_lshl_add_u64 takes shifts 0..4 only (a larger
+// immediate is silently truncated: it broke parity when this was tried with 11).
+template <int S>
+BH_HD uint64_t lshl_add64(uint64_t a, uint64_t b) {
+    static_assert(S >= 0 && S <= 4, "v_lshl_add_u64 shifts by 0..4");
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(S), "v"(b));
+    return r;
+#else
+    return (a << S) + b;
+#endif
+}
+
 BH_HD uint64_t raw_hash1(int32_t k) {  // src/bloom_filter.cpp:8-20
-    uint64_t x = (uint64_t)(int64_t)k;
-    x = ~x + (x << 15);
+    uint64_t x = (uint64_t)((int64_t)k * 32767 - 1);  // x = ~x + (x << 15)
     x = x ^ (x >> 12);
-    x = x + (x << 2);
+    x = lshl_add64<2>(x, x);                            // x = x + (x << 2)
     x = x ^ (x >> 4);
-    x = x * 2057u;
+    x = (x << 11) + lshl_add64<3>(x, x);                // x = x * 2057
     x = x ^ (x >> 16);
     return x;
 }
 
 BH_HD uint64_t raw_hash2(int32_t k) {  // src/bloom_filter.cpp:22-34
-    uint64_t x = (uint64_t)(int64_t)k;
-    x = (x + 0x7ed55d16u) + (x << 12);
+    uint64_t x = (uint64_t)((int64_t)k * 4097 + 0x7ed55d16);  // (x + 0x7ed55d16) + (x << 12)
     x = (x ^ 0xc761c23cu) ^ (x >> 19);
     x = (x + 0x165667b1u) + (x << 5);
     x = (x + 0xd3a2646cu) ^ (x << 9);
@@ -50,7 +71,7 @@ BH_HD uint64_t raw_hash2(int32_t k) {  // src/bloom_filter.cpp:22-34
 BH_HD uint64_t raw_hash3(int32_t k) {  // src/bloom_filter.cpp:36-47
     uint64_t x = (uint64_t)(int64_t)k;
     x = (x ^ 61u) ^ (x >> 16);
-    x = x + (x << 3);
+    x = lshl_add64<3>(x, x);                            // x = x + (x << 3)
     x = x ^ (x >> 4);
     x = x * 0x27d4eb2du;
     x = x ^ (x >> 15);
