@@ -1153,9 +1153,13 @@ hipError_t launch_run_meta(const KeySpan &ks, int32_t *meta, hipStream_t stream)
 hipError_t launch_route(const KeySpan &ks, const RouteTable &t, uint64_t *cand, size_t nw,
                         int32_t *first, int32_t *page, hipStream_t stream) {
     if (nw == 0) return hipSuccess;
-    const unsigned grid = grid_for(nw, kRouteBlock / 64, 16384);
     const size_t lds = (size_t)t.total_fences * 4;
     const bool in_lds = lds <= kRouteLdsFenceBytes;
+    // Every workgroup stages all fences in LDS: a grid-stride loop over a
+    // few workgroups per CU amortises that (16384 workgroups x 22 KB of
+    // fences at C3 was 360 MB of L2 reads, most of the kernel's time).
+    const unsigned cap = in_lds ? 4u * (unsigned)device_cu_count() : 16384u;
+    const unsigned grid = grid_for(nw, kRouteBlock / 64, cap);
 #define ROUTE_LAUNCH(L, F) \
     k_route<L, F><<<grid, kRouteBlock, F ? lds : 0, stream>>>(ks, t, cand, nw, first, page)
     if (ks.layout == KEYS_PACKED) {
