@@ -394,7 +394,7 @@ __global__ void __launch_bounds__(kTransposeBlock) k_runs_transpose(
 // ---------------------------------------------------------------------------
 
 constexpr int kApplyBlock = 1024;
-constexpr int kApplyDepth = 4;  // lane-group loads per wave per batch
+constexpr int kApplyDepth = 2;  // lane-group loads per wave per batch (tools/ubench.py part*: 2 beat 1, 4, 8, 16 at C2/C4/C5)
 
 // Lanes per tile for pass 2, from the average run length L = kPartTilePos /
 // nbins.  A step of 4G entries per tile; runs longer than a step finish in
@@ -435,7 +435,7 @@ inline int apply_lanes_per_tile(size_t nbins) {
 // launches 0.
 constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2;
 
-template <int MODE, int G, int ABLATE = 0, int BLOCK = kApplyBlock>
+template <int MODE, int G, int ABLATE = 0, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth>
 __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const uint32_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, uint32_t seg_bits, uint64_t m, uint32_t *__restrict__ words, uint64_t nw32,
@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     constexpr bool PROBE = MODE != kApplyBuild;
     static_assert(G >= 1 && G <= 64 && (64 % G) == 0, "G lanes per tile");
     constexpr int kTPI = 64 / G;                     // tiles per load instruction
-    constexpr int kBatchTiles = kTPI * kApplyDepth;  // tiles per wave batch
+    constexpr int kBatchTiles = kTPI * DEPTH;  // tiles per wave batch
     constexpr uint32_t kStep = 4 * G;                // entries a tile advances per step
     constexpr uint32_t kLastVec = kPartTilePos - 4;
 
@@ -482,9 +482,9 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const int tl = lane / G;                         // this lane's tile in a load group
     const int nbatch = (ntiles + kBatchTiles - 1) / kBatchTiles;
 
-    auto bounds = [&](int j, uint2 (&r)[kApplyDepth]) {
+    auto bounds = [&](int j, uint2 (&r)[DEPTH]) {
 #pragma unroll
-        for (int d = 0; d < kApplyDepth; d++) {
+        for (int d = 0; d < DEPTH; d++) {
             const int t = j * kBatchTiles + d * kTPI + tl;
             if (t < ntiles) {
                 r[d] = make_uint2(run_starts[(size_t)b * ntiles + t],
@@ -576,32 +576,32 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         }
     };
 
-    uint2 r[kApplyDepth];
+    uint2 r[DEPTH];
     if (wave < nbatch) bounds(wave, r);
     for (int j = wave; j < nbatch; j += (BLOCK / 64)) {
-        int t[kApplyDepth];
-        uint32_t e[kApplyDepth];
-        uint4 v[kApplyDepth];
+        int t[DEPTH];
+        uint32_t e[DEPTH];
+        uint4 v[DEPTH];
 #pragma unroll
-        for (int d = 0; d < kApplyDepth; d++) {
+        for (int d = 0; d < DEPTH; d++) {
             t[d] = min(j * kBatchTiles + d * kTPI + tl, ntiles - 1);
             e[d] = (r[d].x & ~3u) + sub4;
             v[d] = load(t[d], min(e[d], kLastVec));
         }
-        uint2 rn[kApplyDepth];
+        uint2 rn[DEPTH];
         const int jn = j + (BLOCK / 64);
         if (jn < nbatch) bounds(jn, rn);
 #pragma unroll
-        for (int d = 0; d < kApplyDepth; d++) apply4(v[d], t[d], min(e[d], kLastVec));
+        for (int d = 0; d < DEPTH; d++) apply4(v[d], t[d], min(e[d], kLastVec));
 #pragma unroll
-        for (int d = 0; d < kApplyDepth; d++) {
+        for (int d = 0; d < DEPTH; d++) {
             for (uint32_t en = e[d] + kStep; __ballot(en < r[d].y) != 0; en += kStep) {
                 const uint32_t ec = min(en, kLastVec);
                 apply4(load(t[d], ec), t[d], ec);
             }
         }
 #pragma unroll
-        for (int d = 0; d < kApplyDepth; d++) r[d] = rn[d];
+        for (int d = 0; d < DEPTH; d++) r[d] = rn[d];
     }
     if constexpr (PROBE) return;
     __syncthreads();

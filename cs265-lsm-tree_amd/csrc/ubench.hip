@@ -155,12 +155,13 @@ extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_
     const uint64_t nw32 = ((m + 63) / 64) * 2;
     const uint32_t sb = ws.seg_bits;
     if (variant == 0) variant = apply_lanes_per_tile(ws.nbins);
-#define UB_APPLY(G, A)                                                                        \
+#define UB_APPLY(G, A) UB_APPLYD(G, A, kApplyDepth)
+#define UB_APPLYD(G, A, D)                                                                    \
     do {                                                                                      \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<kApplyBuild, G, A>), \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<kApplyBuild, G, A, kApplyBlock, D>), \
                                   hipFuncAttributeMaxDynamicSharedMemorySize,                 \
                                   (int)(kSegMaxBits / 8));                                    \
-        k_part_apply<kApplyBuild, G, A><<<nbins, kApplyBlock, sb / 8, s>>>(                         \
+        k_part_apply<kApplyBuild, G, A, kApplyBlock, D><<<nbins, kApplyBlock, sb / 8, s>>>(         \
             pos, run_starts, ntiles, nbins, sb, m, words, nw32, 0, nullptr, StackTable{});    \
     } while (0)
     switch (variant) {
@@ -170,6 +171,14 @@ extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_
         case 16: UB_APPLY(16, 0); break;
         case 32: UB_APPLY(32, 0); break;
         case 64: UB_APPLY(64, 0); break;
+        case 402: UB_APPLYD(2, 0, 2); break;   // 400 + G: depth 2, 500 + G: depth 1
+        case 404: UB_APPLYD(4, 0, 2); break;
+        case 408: UB_APPLYD(8, 0, 2); break;
+        case 416: UB_APPLYD(16, 0, 2); break;
+        case 502: UB_APPLYD(2, 0, 1); break;
+        case 504: UB_APPLYD(4, 0, 1); break;
+        case 508: UB_APPLYD(8, 0, 1); break;
+        case 516: UB_APPLYD(16, 0, 1); break;
         case 102: UB_APPLY(2, 1); break;
         case 104: UB_APPLY(4, 1); break;
         case 108: UB_APPLY(8, 1); break;
@@ -178,6 +187,7 @@ extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_
         default: return -22;
     }
 #undef UB_APPLY
+#undef UB_APPLYD
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

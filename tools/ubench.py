@@ -78,7 +78,7 @@ def part_ablation(n=16_777_216, bpe=10.0):
         LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(), rs.data_ptr(),
                             s.cuda_stream)
         torch.cuda.synchronize()
-        for batch in (0, 2, 4, 8, 16, 32, 104, 108, 116, 0):
+        for batch in (0, 4, 8, 16, 402, 404, 408, 416, 502, 504, 508, 516, 0):
             for _ in range(2):
                 rc = LIB.ubench_part_apply(batch, pos.data_ptr(), rs.data_ptr(), keys.numel(), m,
                                            words.data_ptr(), s.cuda_stream)
