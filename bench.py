@@ -62,6 +62,62 @@ def cpu_baseline(keys, m, reps=5):
                       f"1 thread, median of {reps} ({t:.3f} s each)"}
 
 
+def cpu_baseline_detail(keys, m):
+    """SURVEY §8d's CPU plan beside the headline baseline: the oracle's C
+    restatement at the reference's own flags (-O0 -g) and at -O2; one filter
+    per thread (per-run builds, as C5) and a threaded C3 probe, on T host
+    threads.  Bounded samples: a few seconds of CPU in all."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from bloom_oracle import COracle
+    from bloomhip import workloads as W
+    import numpy as np
+    T = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+
+    def med(fn, reps=3):
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+
+    def parallel(fns):
+        th = [threading.Thread(target=f) for f in fns]   # ctypes drops the GIL
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return time.perf_counter() - t0
+
+    C0, C2 = COracle("O0"), COracle()
+    sample = keys[:1 << 22]
+    t_o0 = med(lambda: C0.build(m, sample))
+    t_par = min(parallel([lambda: C2.build(m, keys) for _ in range(T)]) for _ in range(2))
+    gets, levels = W.c3()
+    filt = [(C2.build(mm, k), mm) for _, k, mm in levels]
+    parts = np.array_split(gets, T)
+
+    def probe_part(p):
+        for w, mm in filt:
+            C2.test(w, mm, p)
+    t_probe = min(parallel([lambda p=p: probe_part(p) for p in parts]) for _ in range(2))
+    return {"cpu_model": model, "host_cpus": os.cpu_count(), "threads": T,
+            "build_O0_1thread_gkeys_s": round(sample.size / t_o0 / 1e9, 5),
+            "build_O0_sample": f"first {sample.size} C2 keys, oracle at -O0 -g, median of 3",
+            "build_O2_per_run_threads_gkeys_s": round(T * keys.size / t_par / 1e9, 4),
+            "build_O2_per_run_threads": f"{T} C2-sized filters, one per thread, best of 2",
+            "probe_c3_O2_threads_gkeys_s": round(gets.size / t_probe / 1e9, 4),
+            "probe_c3_O2_threads": f"16.8M C3 GETs x 5 level filters, keys split over {T} threads"}
+
+
 def pmc_traffic(workload):
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(path):
@@ -311,6 +367,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         cpu = cpu_baseline(keys, m)
+        if not args.no_extras:
+            log("cpu baseline detail ...")
+            extras["cpu_baseline_detail"] = cpu_baseline_detail(keys, m)
 
     if rank != 0:
         if dist:

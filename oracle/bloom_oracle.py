@@ -117,19 +117,20 @@ def unpack_bools(packed: np.ndarray, n: int) -> np.ndarray:
 # --------------------------------------------------------------------------
 # C restatement (oracle/bloom_oracle.c) via ctypes.
 # --------------------------------------------------------------------------
-def build_c_oracle(force: bool = False) -> str:
+def build_c_oracle(force: bool = False, lib: str = "liboracle.so") -> str:
     src = os.path.join(HERE, "bloom_oracle.c")
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
-        subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
-    return LIB_PATH
+    path = os.path.join(HERE, lib)
+    if force or not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE, lib])
+    return path
 
 
 class COracle:
-    """ctypes view of oracle/bloom_oracle.c."""
+    """ctypes view of oracle/bloom_oracle.c.  flags="O0" loads the build at the
+    reference Makefile's own flags (-O0 -g, Makefile:4), for the CPU baseline."""
 
-    def __init__(self):
-        build_c_oracle()
-        L = ctypes.CDLL(LIB_PATH)
+    def __init__(self, flags: str = "O2"):
+        L = ctypes.CDLL(build_c_oracle(lib="liboracle_O0.so" if flags == "O0" else "liboracle.so"))
         P = ctypes.c_void_p
         L.bo_m_bits.argtypes = [ctypes.c_int64, ctypes.c_float, ctypes.POINTER(ctypes.c_uint64)]
         L.bo_m_bits.restype = ctypes.c_int
