@@ -26,6 +26,10 @@ def per_kernel(d):
         base = name.split("<")[0]
         if base not in BUILD_KERNELS or "<true" in name:  # PROBE / SLOTS variants
             continue
+        if base == "k_part_apply" and not name.startswith("k_part_apply<0"):  # probe modes
+            continue
+        if base == "k_part_bin" and ", true," in name.split(">")[0].split("<", 1)[1][:20]:
+            continue  # SLOTS (probe) variant
         if base not in best or int(grid) > best[base][0]:
             best[base] = (int(grid), name, ctrs)
     return best
