@@ -73,6 +73,40 @@ __global__ void ub_rawhash(int iters, uint32_t *sink) {
     if (acc == 0x12345678u) sink[0] = (uint32_t)acc;
 }
 
+// VALU / LDS overlap probe: waves of the first `valu_waves` of each 16-wave
+// workgroup run the hash+mod loop, the others random LDS ds_add_rtn (mode 0:
+// both, 1: hash waves only (others exit), 2: LDS waves only).
+template <int OP>  // LDS op of the non-hashing waves: 0 ds_add_rtn, 1 ds_write, 2 ds_read
+__global__ void __launch_bounds__(1024) ub_mixed(ModParams mp, int valu_waves, int mode,
+                                                 int hash_iters, int lds_iters, uint32_t *sink) {
+    extern __shared__ uint32_t seg[];
+    for (int i = threadIdx.x; i < 16384; i += blockDim.x) seg[i] = 0;
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    if (wave < valu_waves) {
+        if (mode == 2) return;
+        uint32_t acc = 0;
+        int32_t k = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u);
+        for (int i = 0; i < hash_iters; i++) {
+            acc ^= mod_fast(raw_hash1(k), mp) + mod_fast(raw_hash2(k), mp) + mod_fast(raw_hash3(k), mp);
+            k += 0x9E3779B9;
+        }
+        if (acc == 0x12345678u) sink[0] = acc;
+    } else {
+        if (mode == 1) return;
+        uint32_t s = 0x9E3779B9u ^ (blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u;
+        uint32_t acc = 0;
+        for (int i = 0; i < lds_iters; i++) {
+            s += 0x9E3779B9u;  // 1 VALU per op (a Weyl sequence), so the LDS waves stay LDS-bound
+            const uint32_t r = s;
+            if constexpr (OP == 0) acc += atomicAdd(&seg[r >> 18], 1u);  // pass 1's ranks
+            else if constexpr (OP == 1) seg[r >> 18] = r;                  // the scatter
+            else acc += seg[r >> 18];                                      // offset reads
+        }
+        if (acc == 0x12345678u) sink[0] = acc;
+    }
+}
+
 __global__ void ub_stream(const uint4 *buf, size_t n16, uint32_t *sink) {
     uint32_t acc = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16;
@@ -99,6 +133,18 @@ extern "C" int ubench_run(int which, void *dbuf, size_t bytes, uint64_t m, int g
         case 4: ub_hash<<<grid, block, 0, s>>>(make_mod_params(m), iters, sink); break;
         case 5: ub_rawhash<<<grid, block, 0, s>>>(iters, sink); break;
         case 6: ub_stream<<<grid, block, 0, s>>>(reinterpret_cast<const uint4 *>(dbuf), bytes / 16 - 1, sink); break;
+        case 10: case 11: case 12:  // block = waves doing VALU (of 16), iters = hash iters
+            ub_mixed<0><<<grid, 1024, 65536, s>>>(make_mod_params(167772160), block, which - 10,
+                                                  iters, iters * 6, sink);
+            break;
+        case 20: case 21: case 22:
+            ub_mixed<1><<<grid, 1024, 65536, s>>>(make_mod_params(167772160), block, which - 20,
+                                                  iters, iters * 6, sink);
+            break;
+        case 30: case 31: case 32:
+            ub_mixed<2><<<grid, 1024, 65536, s>>>(make_mod_params(167772160), block, which - 30,
+                                                  iters, iters * 6, sink);
+            break;
         default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -212,8 +212,25 @@ def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
                           "us": round(a.elapsed_time(b) / 20 * 1e3, 1)}), flush=True)
 
 
+def mixed():
+    """Can LDS atomics and VALU hashing overlap on a CU?  Some of 16 waves
+    hash, the rest do random ds_add_rtn: time both together vs each alone."""
+    buf = torch.zeros(1 << 20, dtype=torch.int32, device="cuda")
+    nb = buf.numel() * 4
+    for base, lds_op in ((10, "ds_add_rtn"), (20, "ds_write"), (30, "ds_read")):
+      for vw in (8, 4, 12):
+        t = {}
+        for mode, name in ((0, "both"), (1, "valu only"), (2, "lds only")):
+            t[name] = timeit(base + mode, buf, nb, 0, 512, vw, 64)
+        print(json.dumps({"op": "valu/lds overlap", "lds_op": lds_op, "valu_waves": vw,
+                          **{k: round(v * 1e3, 1) for k, v in t.items()},
+                          "sum": round((t["valu only"] + t["lds only"]) * 1e3, 1)}), flush=True)
+
+
 def main():
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "mixed":
+        return mixed()
     if len(sys.argv) > 1 and sys.argv[1] == "stack":
         stack_ablation()
         return stack_ablation((0, 1, 2, 3))
