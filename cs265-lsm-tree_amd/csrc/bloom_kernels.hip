@@ -834,19 +834,36 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
         }
         int32_t pg = -1;
         if (fr >= 0) {
-            // upper_bound(fences, k): 8-ary rounds (7 independent LDS reads
-            // each) while the range is wide, then binary steps: 4 dependent
-            // rounds instead of 12 for a 4096-fence run.  Invariant: fences
-            // [0, lo) are <= k, fences [hi, n) are > k.
-            uint32_t lo = 0, hi = t.nfences[fr];
-            while (hi - lo > 16) {
-                const uint32_t w = hi - lo;
-                uint32_t c = 0;
-#pragma unroll
-                for (uint32_t j = 1; j < 8; j++) c += fence(fr, lo + w * j / 8) <= k ? 1u : 0u;
-                const uint32_t nlo = c ? lo + w * c / 8 + 1 : lo;
-                hi = c < 7 ? lo + w * (c + 1) / 8 : hi;
-                lo = nlo;
+            // upper_bound(fences, k).  A run's keys are sorted and, in an LSM,
+            // close to uniform, so interpolation steps narrow the range in
+            // few LDS reads; a binary search finishes (and bounds the worst
+            // case).  Invariant: fences [0, lo) are <= k, [hi, n) are > k.
+            const uint32_t n = t.nfences[fr];
+            uint32_t lo = 0, hi = n;
+            if (n > 16) {
+                int32_t a = fence(fr, 0), z = fence(fr, n - 1);
+                if (k < a) {
+                    hi = 0;
+                } else if (k >= z) {
+                    lo = n;
+                } else {  // a <= k < z: the answer is in [1, n - 1]
+                    lo = 1;
+                    hi = n - 1;
+                    for (int it = 0; it < 3 && hi - lo > 8; it++) {
+                        // a = a fence <= k just below lo, z = a fence > k at/after hi
+                        const float frac = (float)((double)k - a) / (float)((double)z - a);
+                        uint32_t g = lo + (uint32_t)(frac * (float)(hi - lo));
+                        g = min(max(g, lo), hi - 1);
+                        const int32_t fg = fence(fr, g);
+                        if (fg <= k) {
+                            lo = g + 1;
+                            a = fg;
+                        } else {
+                            hi = g;
+                            z = fg;
+                        }
+                    }
+                }
             }
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
