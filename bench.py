@@ -199,6 +199,48 @@ def route_c3(torch, bh, steps, warmup):
             "keys_with_candidate": routed}
 
 
+def probe_c3_sharded(torch, bh, dist, rank, world, steps, warmup, coll_dev):
+    """SURVEY §8e's probe side at N > 1: every rank holds the five C3 level
+    filters (built locally from the same run keys: replicas, no collective)
+    and probes its contiguous slice of the 16.8M GETs (shard.probe_slice).
+    Aggregate rate = all GETs / max over ranks of the timed region."""
+    import numpy as np
+    from bloomhip import shard
+    from bloomhip import workloads as W
+    gets, levels = W.c3()
+    filters = []
+    for lvl, keys, m in levels:
+        f = bh.BloomFilter(m, device=torch.cuda.current_device())
+        f.set_batch(keys)
+        filters.append(f)
+    lo, hi = shard.probe_slice(gets.size, rank, world)
+    dg = torch.from_numpy(gets[lo:hi]).cuda()
+    nw = (hi - lo + 63) // 64
+    dout = torch.empty((len(filters), max(nw, 1)), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream()
+    for _ in range(warmup):
+        bh.test_batch(filters, dg, out=dout, stream=s)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        bh.test_batch(filters, dg, out=dout, stream=s)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = shard.max_over_ranks((time.perf_counter() - t0) / steps, dist, device=coll_dev)
+    hits = [int(np.unpackbits(dout[j].cpu().numpy().view(np.uint8)).sum())
+            for j in range(len(filters))] if hi > lo else [0] * len(filters)
+    tot = [int(shard.sum_over_ranks(h, dist, device=coll_dev)) for h in hits]
+    want = None
+    pins_path = os.path.join(ROOT, "tests", "golden", "pins.json")
+    if os.path.exists(pins_path):
+        want = json.load(open(pins_path))["reference"]["c3_hits"]
+    return {"gkeys_s": round(gets.size / el / 1e9, 3), "ms": round(el * 1e3, 4),
+            "keys_per_rank": hi - lo, "hits_per_level": tot,
+            "hits_match_reference": (tot == want) if want is not None else None,
+            "note": "filters replicated per GPU, GET keys sharded contiguously, no data collective"}
+
+
 def compact_fanin(torch, bh, reps):
     """§8f row 3: a fan-in-4 compaction (4 runs x 4M entries, newest first)
     merged on the device and fused with the new run's filter + fence build
@@ -355,6 +397,11 @@ def main():
 
     extras = {}
     cpu = None
+    if world > 1 and not args.no_extras:
+        if rank == 0:
+            log("sharded probe C3 ...")
+        extras["probe_c3_sharded"] = probe_c3_sharded(torch, bh, dist, rank, world,
+                                                      max(5, args.steps // 5), 2, coll_dev)
     if rank == 0 and world == 1 and not args.no_extras:
         log("probe C3 ...")
         extras["probe_c3"] = probe_c3(torch, bh, max(5, args.steps // 5), 2)

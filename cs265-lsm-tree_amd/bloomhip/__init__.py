@@ -58,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "bloomhip_gen_mt19937", "bloomhip_gen_glibc_rand", "bloomhip_gen_puts",
     "bloomhip_gen_workload", "bloomhip_set_batch_run", "bloomhip_set_run_meta",
     "bloomhip_get_run_meta", "bloomhip_route_gets", "bloomhip_save", "bloomhip_load",
-    "bloomhip_build_from_run_file", "bloomhip_compact",
+    "bloomhip_build_from_run_file", "bloomhip_compact", "bloomhip_clone",
 )
 
 
@@ -136,6 +136,7 @@ def _lib():
             "bloomhip_compact": (I, [ctypes.POINTER(P), P, I, I, I, P, ctypes.POINTER(SZ), I, P,
                                      I, P]),
             "bloomhip_save": (I, [P, ctypes.c_char_p]),
+            "bloomhip_clone": (I, [P, I, ctypes.POINTER(P)]),
             "bloomhip_load": (I, [ctypes.c_char_p, I, ctypes.POINTER(P)]),
             "bloomhip_build_from_run_file": (I, [ctypes.c_char_p, U64, ctypes.c_int64,
                                                  ctypes.c_float, I, ctypes.POINTER(P)]),
@@ -246,6 +247,14 @@ class BloomFilter:
                                                    bits_per_entry, device, ctypes.byref(h)),
                "bloomhip_build_from_run_file")
         return cls._adopt(h, device)
+
+    def clone(self, device: int | None = None) -> "BloomFilter":
+        """bloomhip_clone: this filter (bitmap + run metadata) on `device`
+        (peer copy over xGMI between GPUs)."""
+        dev = self.device if device is None else device
+        h = ctypes.c_void_p()
+        _check(_lib().bloomhip_clone(self._h, dev, ctypes.byref(h)), "bloomhip_clone")
+        return BloomFilter._adopt(h, dev)
 
     def save(self, path: str) -> None:
         _check(_lib().bloomhip_save(self._h, os.fsencode(path)), "bloomhip_save")

@@ -950,6 +950,55 @@ int bloomhip_upload(bloomhip_filter *f, const uint64_t *words, size_t nwords, vo
     return BLOOMHIP_OK;
 }
 
+int bloomhip_clone(const bloomhip_filter *src, int device, bloomhip_filter **out) {
+    g_last_error.clear();
+    if (!src || !out) return BLOOMHIP_EINVAL;
+    *out = nullptr;
+    bloomhip_filter *f = nullptr;
+    int rc = bloomhip_create(device, src->m, &f);
+    if (rc) return rc;
+    bloomhip_filter *sm = const_cast<bloomhip_filter *>(src);
+    {
+        DeviceGuard gs(src->device);
+        std::lock_guard<std::mutex> lk(sm->mu);
+        // the source's queued work may be on any stream: wait for the device
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess && !sm->pending_clear) {
+            // xGMI peer copy between devices, a D2D copy on one device
+            e = src->device == device
+                    ? hipMemcpy(f->d_words, src->d_words, src->nwords64 * 8,
+                                hipMemcpyDeviceToDevice)
+                    : hipMemcpyPeer(f->d_words, device, src->d_words, src->device,
+                                    src->nwords64 * 8);
+        }
+        if (e == hipSuccess && src->d_meta) {
+            std::vector<int32_t> h(src->nfences + 1);
+            e = hipMemcpy(h.data(), src->d_meta, h.size() * 4, hipMemcpyDeviceToHost);
+            if (e == hipSuccess) {
+                f->known_zero = sm->pending_clear || sm->known_zero;
+                f->strategy = src->strategy;
+                f->probe_strategy = src->probe_strategy;
+                rc = bloomhip_set_run_meta(f, h.data() + 1, src->nfences, h[0]);
+            }
+        } else if (e == hipSuccess) {
+            f->known_zero = sm->pending_clear || sm->known_zero;
+            f->strategy = src->strategy;
+            f->probe_strategy = src->probe_strategy;
+        }
+        if (e != hipSuccess) rc = fail_hip(e, "bloomhip_clone copy");
+    }
+    if (rc) {
+        (void)bloomhip_destroy(f);
+        return rc;
+    }
+    if (!f->known_zero) {
+        DeviceGuard gd(device);
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    *out = f;
+    return BLOOMHIP_OK;
+}
+
 int bloomhip_sync(const bloomhip_filter *f, void *stream) {
     g_last_error.clear();
     if (!f) return BLOOMHIP_EINVAL;

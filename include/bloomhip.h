@@ -201,6 +201,12 @@ int bloomhip_is_set(const bloomhip_filter *f, int32_t key, int *hit_out);
 int bloomhip_download(const bloomhip_filter *f, uint64_t *words, size_t nwords, void *stream);
 int bloomhip_upload(bloomhip_filter *f, const uint64_t *words, size_t nwords, void *stream);
 
+/* A copy of filter src (bitmap, run metadata, strategies) on `device`: a
+ * peer copy over xGMI between GPUs, a device-to-device copy on one GPU.  The
+ * probe side of per-run sharding: each GPU holds replicas of the
+ * runs' filters and probes its own slice of the GET keys.  Synchronous. */
+int bloomhip_clone(const bloomhip_filter *src, int device, bloomhip_filter **out);
+
 /* Wait for all work queued on `stream` (NULL: the default stream). */
 int bloomhip_sync(const bloomhip_filter *f, void *stream);
 

@@ -51,6 +51,76 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def test_probe_slices_partition_the_gets():
+    for n in (0, 1, 63, 64, 65, 16_777_216, 1_000_003):
+        for world in (1, 2, 3, 4, 8):
+            sl = [shard.probe_slice(n, r, world) for r in range(world)]
+            assert sl[0][0] == 0 and sl[-1][1] == n
+            for (a, b), (c, d) in zip(sl, sl[1:]):
+                assert b == c and a <= b
+            for a, b in sl[:-1]:
+                assert a % 64 == 0 and b % 64 == 0     # packed words never straddle ranks
+    with pytest.raises(ValueError):
+        shard.probe_slice(10, 2, 2)
+
+
+def _probe_worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path[:0] = [p for p in os.environ.get("BLOOMHIP_TEST_PATH", "").split(":") if p]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bloomhip as bh
+        from bloom_oracle import COracle
+        C = COracle()
+        # every rank holds replicas of the same run filters ...
+        filters = []
+        for r in range(3):
+            keys, m = _run_keys(r)
+            filters.append((C.build(m, keys), m))
+        gets = bh.gen_puts(777, 50_017)
+        gets[:20_000] = _run_keys(1)[0][:20_000]
+        # ... and probes its own contiguous slice of the GETs
+        lo, hi = shard.probe_slice(gets.size, rank, world)
+        rows = [C.test(w, m, gets[lo:hi]) for w, m in filters]
+        parts = [None] * world
+        dist.all_gather_object(parts, (lo, hi, rows))
+        hits = shard.sum_over_ranks(sum(int(np.unpackbits(r.view(np.uint8)).sum()) for r in rows),
+                                    dist)
+        q.put((rank, parts, hits))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_probe(coracle):
+    """Probe side of §8e: replicated filters, GETs sharded by probe_slice; the
+    ranks' packed rows concatenate into the single-process result."""
+    import bloomhip as bh
+    world = 2
+    port = _free_port()
+    os.environ["BLOOMHIP_TEST_PATH"] = ":".join(sys.path[:3])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_probe_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    gets = bh.gen_puts(777, 50_017)
+    gets[:20_000] = _run_keys(1)[0][:20_000]
+    for rank, parts, hits in res:
+        total = 0
+        for r in range(3):
+            keys, m = _run_keys(r)
+            want = coracle.test(coracle.build(m, keys), m, gets)
+            got = np.concatenate([p[2][r] for p in parts])
+            assert np.array_equal(got, want), r
+            total += int(np.unpackbits(want.view(np.uint8)).sum())
+        assert hits == total
+
+
 def test_assignment_is_a_partition():
     for world in (1, 2, 4, 8):
         runs = [r for k in range(world) for r in shard.runs_for_rank(N_RUNS, k, world)]
