@@ -264,7 +264,9 @@ def _stack_case(coracle, ms, probe_keys, strategies=None, stride=4, seed=0):
         f.set_batch(keys)
         filters.append(f)
         refs.append((m, coracle.build(m, keys)))
-        probe_keys[j * 1000:(j + 1) * 1000] = keys[:1000]   # some hits per filter
+        lo, hi = j * 1000, min((j + 1) * 1000, probe_keys.size)
+        if lo < hi:
+            probe_keys[lo:hi] = keys[:hi - lo]   # some hits per filter
     if stride == 8:
         aos = np.zeros((probe_keys.size, 2), dtype=np.int32)
         aos[:, 0] = probe_keys
@@ -294,6 +296,36 @@ def test_stacked_probe_auto_and_strided(coracle):
     probe = rand_keys(270_000, 78)
     _stack_case(coracle, ms, probe, strategies=[bh.PROBE_AUTO] * 5)
     _stack_case(coracle, ms[:3], rand_keys(263_001, 79), stride=8, seed=7)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 4095, 4097])
+def test_stacked_probe_tiny_and_ragged_batches(coracle, n):
+    """Explicit STACKED on batches smaller than a tile or one tile plus one key."""
+    ms = [40_960 * 4**i for i in range(3)]
+    probe = rand_keys(n, 80 + n)
+    _stack_case(coracle, ms, probe)
+
+
+def test_stacked_probe_with_cleared_and_empty_members(coracle):
+    """A member that was never built and one that was cleared (deferred memset)
+    probe as all-miss rows inside the stack."""
+    ms = [655_360 * 4**i for i in range(4)]
+    filters, refs = [], []
+    for j, m in enumerate(ms):
+        f = bh.BloomFilter(m)
+        f.set_probe_strategy(bh.PROBE_STACKED)
+        keys = rand_keys(30_000, 300 + j)
+        if j != 1:
+            f.set_batch(keys)
+        if j == 2:
+            f.clear()
+        filters.append(f)
+        refs.append((m, coracle.build(m, keys) if j in (0, 3) else np.zeros((m + 63) // 64, np.uint64)))
+    probe = rand_keys(280_001, 81)
+    got = bh.test_batch(filters, probe)
+    for j, (m, w) in enumerate(refs):
+        assert (got[j] == coracle.test(w, m, probe)).all(), j
+    assert not got[1].any() and not got[2].any()
 
 
 def test_stacked_probe_profile_slot():
