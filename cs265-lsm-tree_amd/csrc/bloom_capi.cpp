@@ -286,9 +286,10 @@ int strategy_supported(const bloomhip_filter *f, int strategy) {
 // plan_segments / plan_stack): the position/run buffers of `w` grown to fit.
 int partition_buffers(Workspace *w, size_t n, hipStream_t s, PartitionWorkspace *ws_inout) {
     PartitionWorkspace ws = *ws_inout;
-    ws.ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
+    if (ws.tile_keys == 0) ws.tile_keys = choose_tile_keys(ws.nbins);
+    ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->pos), &w->pos_bytes,
-                         ws.ntiles * (size_t)kPartTilePos * 4, s));
+                         ws.ntiles * (size_t)ws.tile_keys * 3 * 4, s));
     const size_t table = ws.ntiles * (ws.nbins + 1);  // run starts, both layouts
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->runs), &w->runs_bytes, table * 2 * 4, s));
     ws.pos = w->pos;
@@ -311,9 +312,9 @@ int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
 // The partitioned probe's result bytes and slots, grown to fit ws.
 int probe_buffers(Workspace *w, const PartitionWorkspace &ws, hipStream_t s) {
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->res), &w->res_bytes,
-                         ws.ntiles * (size_t)kPartTilePos, s));
+                         ws.ntiles * (size_t)ws.tile_keys * 3, s));
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->slots), &w->slots_bytes,
-                         ws.ntiles * 3 * kPartTileKeys * sizeof(uint16_t), s));
+                         ws.ntiles * 3 * (size_t)ws.tile_keys * sizeof(uint16_t), s));
     return BLOOMHIP_OK;
 }
 

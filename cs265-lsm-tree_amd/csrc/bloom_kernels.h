@@ -104,7 +104,19 @@ struct PartitionWorkspace {
     uint32_t group;        // sub-segments per pass-2 segment
     uint32_t nsub;         // pass-1 sub-segments
     uint32_t seg_bits;     // S = group << sub_shift
+    uint32_t tile_keys;    // keys per pass-1 tile: kPartTileKeys, or twice that (0 = default)
 };
+
+// Keys per pass-1 tile for a batch sorted into nbins segments: short runs
+// (> 1024 segments: under 12 entries per segment and 4096-key tile) make
+// pass 2 line-bound, so such batches sort 8192-key tiles (one 1024-thread
+// workgroup per CU) and get runs twice as long (tools/ubench.py part_c4).
+inline uint32_t choose_tile_keys(size_t nbins) {
+    return nbins > 1024 ? 2 * (uint32_t)kPartTileKeys : (uint32_t)kPartTileKeys;
+}
+inline size_t tile_keys_of(const PartitionWorkspace &ws) {
+    return ws.tile_keys ? ws.tile_keys : kPartTileKeys;
+}
 
 // Geometry of a stacked probe (seg_bits = w): false when no w = g << s with
 // w | gcd_m, nf * w bits <= kSegMaxBits and <= kPartMaxBins sub-segments

@@ -132,7 +132,6 @@ __global__ void __launch_bounds__(kBlock) k_build_lds(KeySpan ks, ModParams mp,
 // position got in the sorted tile: slots[(tile*3 + h)*kPartTileKeys + key].
 // ---------------------------------------------------------------------------
 constexpr int kMaxBins = (int)kPartMaxBins;
-constexpr int kScanPer = (kMaxBins + 1 + kPartBlock - 1) / kPartBlock;  // entries per thread
 
 // Workgroup barrier that waits for this wave's LDS operations only.
 __device__ __forceinline__ void lds_barrier() {
@@ -144,13 +143,13 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
-template <int LAYOUT>
+template <int LAYOUT, int TB>
 __device__ __forceinline__ void load_tile_keys(const KeySpan &ks, size_t tile, int tid,
                                                int32_t (&k)[kPartKPT]) {
-    const size_t tile0 = tile * kPartTileKeys;
+    const size_t tile0 = tile * (size_t)(TB * kPartKPT);
 #pragma unroll
     for (int j = 0; j < kPartKPT; j++) {
-        const size_t i = tile0 + (size_t)j * kPartBlock + tid;
+        const size_t i = tile0 + (size_t)j * TB + tid;
         if (i < ks.n) {
             if constexpr (LAYOUT == KEYS_PACKED) k[j] = reinterpret_cast<const int32_t *>(ks.base)[i];
             else k[j] = load_key(ks, i);
@@ -189,16 +188,22 @@ __device__ __forceinline__ size_t part_tile(size_t k, size_t ntiles) {
 // COLS = true: straight into the segment-major table runs[b * ntiles + tile];
 // COLS = false: into the tile-major runs[tile * (nbins + 1) + b], for
 // k_runs_transpose (large tables: see there).
-template <int LAYOUT, int ABLATE = 0, bool SLOTS = false, bool COLS = true>
-__global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParams mp,
+template <int LAYOUT, int ABLATE = 0, bool SLOTS = false, bool COLS = true, int TB = kPartBlock>
+__global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
                                                          uint32_t *__restrict__ pos_out,
                                                          uint32_t *__restrict__ runs,
                                                          int nbins, int nsub, int sub_shift,
                                                          int group, size_t ntiles,
                                                          uint16_t *__restrict__ slots) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_sorted[kPartTilePos];
+    // tile = TB * kPartKPT keys
+    constexpr int kTileKeys = TB * kPartKPT;
+    constexpr int kTilePos = 3 * kTileKeys;
+    constexpr int kScanPer = (kMaxBins + 1 + TB - 1) / TB;  // scan entries per thread
+    // static LDS even for the 96 KiB of an 8192-key tile (gfx950 takes it);
+    // dynamic LDS or a pointer to it made the compiler spill registers here
+    __shared__ __attribute__((aligned(16))) uint32_t s_sorted[kTilePos];
     __shared__ uint32_t s_hist[kMaxBins + 1];
-    __shared__ uint32_t s_wsum[kPartBlock / 64];
+    __shared__ uint32_t s_wsum[TB / 64];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -211,10 +216,10 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
     // Those loads are issued after the run-start stores for that reason.
     auto do_tile = [&](auto full_c, size_t tile, size_t next) {
         constexpr bool FULL = decltype(full_c)::value;
-        const size_t tile0 = tile * kPartTileKeys;
-        const int tile_keys = FULL ? (int)kPartTileKeys : (int)min((size_t)kPartTileKeys, ks.n - tile0);
-        auto live = [&](int j) { return FULL || j * kPartBlock + tid < tile_keys; };
-        for (int b = tid; b <= nsub; b += kPartBlock) s_hist[b] = 0;
+        const size_t tile0 = tile * kTileKeys;
+        const int tile_keys = FULL ? (int)kTileKeys : (int)min((size_t)kTileKeys, ks.n - tile0);
+        auto live = [&](int j) { return FULL || j * TB + tid < tile_keys; };
+        for (int b = tid; b <= nsub; b += TB) s_hist[b] = 0;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
 
         // 1. positions, and each one's rank inside its sub-segment (LDS
@@ -244,7 +249,7 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
 #pragma unroll
             for (int j = 0; j < kPartKPT * 3; j++) acc ^= pos[j];
             if (acc == 0x9E3779B9u) pos_out[tid] = acc;
-            if (next < ntiles) load_tile_keys<LAYOUT>(ks, next, tid, knext);
+            if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
             return;
         }
         lds_barrier();
@@ -280,14 +285,14 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
         }
         lds_barrier();
         if constexpr (COLS) {
-            for (int b = tid; b <= nbins; b += kPartBlock)
+            for (int b = tid; b <= nbins; b += TB)
                 runs[(size_t)b * ntiles + tile] = s_hist[b == nbins ? nsub : b * group];
         } else {
             uint32_t *row = runs + tile * (size_t)(nbins + 1);
-            for (int b = tid; b <= nbins; b += kPartBlock)
+            for (int b = tid; b <= nbins; b += TB)
                 row[b] = s_hist[b == nbins ? nsub : b * group];
         }
-        if (next < ntiles) load_tile_keys<LAYOUT>(ks, next, tid, knext);
+        if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
 
         if constexpr (ABLATE < 2) {
             // 3. scatter into the LDS image sorted by sub-segment: all 24
@@ -302,7 +307,7 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
                     for (int h = 0; h < 3; h++) {
                         s_sorted[slot[3 * j + h]] = pos[3 * j + h];  // full position
                         if constexpr (SLOTS)
-                            slots[(tile * 3 + h) * kPartTileKeys + j * kPartBlock + tid] =
+                            slots[(tile * 3 + h) * kTileKeys + j * TB + tid] =
                                 (uint16_t)slot[3 * j + h];
                     }
                 }
@@ -312,27 +317,27 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
 
         if constexpr (ABLATE == 0) {
             // 4. the sorted tile goes out with 16-byte stores.
-            uint32_t *dst = pos_out + tile * (size_t)kPartTilePos;
+            uint32_t *dst = pos_out + tile * (size_t)kTilePos;
             if constexpr (FULL) {
                 // exactly kStores unconditional stores per thread
-                constexpr int kStores = kPartTilePos / 4 / kPartBlock;
-                static_assert(kStores * 4 * kPartBlock == kPartTilePos, "whole 16-B stores");
+                constexpr int kStores = kTilePos / 4 / TB;
+                static_assert(kStores * 4 * TB == kTilePos, "whole 16-B stores");
                 uint4 v[kStores];
 #pragma unroll
                 for (int r = 0; r < kStores; r++)
-                    v[r] = reinterpret_cast<const uint4 *>(s_sorted)[r * kPartBlock + tid];
+                    v[r] = reinterpret_cast<const uint4 *>(s_sorted)[r * TB + tid];
 #pragma unroll
                 for (int r = 0; r < kStores; r++)
-                    reinterpret_cast<uint4 *>(dst)[r * kPartBlock + tid] = v[r];
+                    reinterpret_cast<uint4 *>(dst)[r * TB + tid] = v[r];
             } else {
                 const int npos = tile_keys * 3;
                 const int nq = npos / 4;
-                for (int q = tid; q < nq; q += kPartBlock)
+                for (int q = tid; q < nq; q += TB)
                     reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(s_sorted)[q];
-                for (int e = nq * 4 + tid; e < npos; e += kPartBlock) dst[e] = s_sorted[e];
+                for (int e = nq * 4 + tid; e < npos; e += TB) dst[e] = s_sorted[e];
                 // the short last tile: pad with a position no segment holds,
                 // since pass 2 reads whole 16-B vectors and past run ends
-                for (int e = npos + tid; e < kPartTilePos; e += kPartBlock) dst[e] = 0xFFFFFFFFu;
+                for (int e = npos + tid; e < kTilePos; e += TB) dst[e] = 0xFFFFFFFFu;
             }
         } else if constexpr (ABLATE == 1) {
             if (s_sorted[tid] == 0xFFFFFFFFu) pos_out[tid] = 0;
@@ -341,9 +346,9 @@ __global__ void __launch_bounds__(kPartBlock, 4) k_part_bin(KeySpan ks, ModParam
 
     // Full tiles in the loop; the short last tile (index ntiles - 1, always
     // in a block's final round) after it, so the loop sees only FULL.
-    const size_t nfull = ks.n / kPartTileKeys;
+    const size_t nfull = ks.n / kTileKeys;
     size_t tile = part_tile(0, ntiles);
-    if (tile < ntiles) load_tile_keys<LAYOUT>(ks, tile, tid, kcur);
+    if (tile < ntiles) load_tile_keys<LAYOUT, TB>(ks, tile, tid, kcur);
     size_t round = 0;
     for (; tile < nfull; round++) {
         const size_t next = part_tile(round + 1, ntiles);
@@ -401,8 +406,8 @@ constexpr int kApplyDepth = 2;  // lane-group loads per wave per batch (tools/ub
 // the wave-uniform tail loop.  Measured on MI355X (tools/ubench.py part*):
 // G = 8 beats G = 16 even at L = 48 (C2), G = 4 ~ G = 8 at L = 4 (C4), G = 2
 // is always worse (its loads cover too few bytes per lane group).
-inline int apply_lanes_per_tile(size_t nbins) {
-    const size_t L = kPartTilePos / (nbins ? nbins : 1);
+inline int apply_lanes_per_tile(size_t nbins, size_t tile_pos = kPartTilePos) {
+    const size_t L = tile_pos / (nbins ? nbins : 1);
     if (L < 10) return 4;
     if (L < 96) return 8;
     if (L < 192) return 16;
@@ -435,7 +440,8 @@ inline int apply_lanes_per_tile(size_t nbins) {
 // launches 0.
 constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2;
 
-template <int MODE, int G, int ABLATE = 0, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth>
+template <int MODE, int G, int ABLATE = 0, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth,
+          int TILE_POS = kPartTilePos>
 __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const uint32_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, uint32_t seg_bits, uint64_t m, uint32_t *__restrict__ words, uint64_t nw32,
@@ -445,7 +451,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     constexpr int kTPI = 64 / G;                     // tiles per load instruction
     constexpr int kBatchTiles = kTPI * DEPTH;  // tiles per wave batch
     constexpr uint32_t kStep = 4 * G;                // entries a tile advances per step
-    constexpr uint32_t kLastVec = kPartTilePos - 4;
+    constexpr uint32_t kLastVec = TILE_POS - 4;
 
     const uint32_t seg_words = seg_bits / 32;
     extern __shared__ __attribute__((aligned(16))) uint32_t seg[];
@@ -498,10 +504,10 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         if constexpr (ABLATE == 3) {
             typedef uint32_t v4u __attribute__((ext_vector_type(4)));
             const v4u x = __builtin_nontemporal_load(
-                reinterpret_cast<const v4u *>(pos + (size_t)t * kPartTilePos + e));
+                reinterpret_cast<const v4u *>(pos + (size_t)t * TILE_POS + e));
             return make_uint4(x[0], x[1], x[2], x[3]);
         }
-        return *reinterpret_cast<const uint4 *>(pos + (size_t)t * kPartTilePos + e);
+        return *reinterpret_cast<const uint4 *>(pos + (size_t)t * TILE_POS + e);
     };
     auto apply1 = [&](uint32_t v, int t, uint32_t e) {
         const uint32_t o = v - base;
@@ -510,7 +516,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             (void)t; (void)e;
         } else if (o < lim) {
             if constexpr (PROBE) {  // (ABLATE builds only; apply4 handles probes)
-                res[(size_t)t * kPartTilePos + e] = (seg[o >> 5] >> (o & 31)) & 1u;
+                res[(size_t)t * TILE_POS + e] = (seg[o >> 5] >> (o & 31)) & 1u;
             } else {
                 (void)t; (void)e;
                 atomicOr(&seg[o >> 5], 1u << (o & 31));
@@ -557,7 +563,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                     bits |= (((w[k] >> (o[k] & 31)) & ok) << (8 * k));
                 }
             }
-            uint8_t *p = res + (size_t)t * kPartTilePos + e;
+            uint8_t *p = res + (size_t)t * TILE_POS + e;
             if constexpr (ABLATE == 2) {
                 asm volatile("" ::"v"(bits), "v"(mask));
                 (void)p;
@@ -726,24 +732,26 @@ __global__ void __launch_bounds__(kProbeLdsBlock) k_probe_lds(KeySpan ks, const 
 // packed 64 keys per u64 by a 64-lane ballot into row rows.row[j] of out.
 constexpr int kCombineBlock = 256;
 
+template <int TILE_KEYS>
 __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, size_t n,
     uint64_t *__restrict__ out, size_t nw, StackTable rows) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_r[kPartTilePos];
+    constexpr int kTilePos = 3 * TILE_KEYS;
+    __shared__ __attribute__((aligned(16))) uint8_t s_r[kTilePos];
     const size_t tile = blockIdx.x;
-    const size_t tile0 = tile * kPartTileKeys;
-    const int tile_keys = (int)min((size_t)kPartTileKeys, n - tile0);
-    const uint4 *src = reinterpret_cast<const uint4 *>(res + tile * (size_t)kPartTilePos);
-    for (int q = threadIdx.x; q < kPartTilePos / 16; q += kCombineBlock)
+    const size_t tile0 = tile * TILE_KEYS;
+    const int tile_keys = (int)min((size_t)TILE_KEYS, n - tile0);
+    const uint4 *src = reinterpret_cast<const uint4 *>(res + tile * (size_t)kTilePos);
+    for (int q = threadIdx.x; q < kTilePos / 16; q += kCombineBlock)
         reinterpret_cast<uint4 *>(s_r)[q] = src[q];
     __syncthreads();
-    const uint16_t *sl = slots + tile * 3 * kPartTileKeys;
+    const uint16_t *sl = slots + tile * 3 * TILE_KEYS;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int j = 0; j < (int)kPartTileKeys / kCombineBlock; j++) {
+    for (int j = 0; j < (int)TILE_KEYS / kCombineBlock; j++) {
         const int key = j * kCombineBlock + (int)threadIdx.x;
         uint32_t hit = 0;
         if (key < tile_keys)
-            hit = s_r[sl[key]] & s_r[sl[kPartTileKeys + key]] & s_r[sl[2 * kPartTileKeys + key]];
+            hit = s_r[sl[key]] & s_r[sl[TILE_KEYS + key]] & s_r[sl[2 * TILE_KEYS + key]];
         const int base = j * kCombineBlock + wave * 64;
         for (int f = 0; f < rows.nf; f++) {
             const uint64_t ballot = __ballot((hit >> f) & 1u);
@@ -879,9 +887,10 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
     }
 }
 
-// Persistent pass-1 grid: two 64-KiB-LDS workgroups per CU.
-inline unsigned part_bin_grid(size_t ntiles) {
-    const size_t g = (size_t)device_cu_count() * 2;
+// Persistent pass-1 grid: two 64-KiB-LDS workgroups per CU for 4096-key
+// tiles, one 112-KiB workgroup for 8192-key tiles.
+inline unsigned part_bin_grid(size_t ntiles, int tb = kPartBlock) {
+    const size_t g = (size_t)device_cu_count() * (tb >= 1024 ? 1 : 2);
     return (unsigned)(ntiles < g ? ntiles : g);
 }
 
@@ -1034,18 +1043,18 @@ bool runs_as_columns(const PartitionWorkspace &ws) {
     return ws.ntiles * (ws.nbins + 1) * 4 <= kColumnTableMaxBytes;
 }
 
-// Pass 1 for a build (SLOTS = false) or a probe (SLOTS = true), then the
-// run-start transpose when the table is large.
-template <bool SLOTS>
-hipError_t launch_bin(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
-                      uint16_t *slots, hipStream_t stream) {
-    const unsigned grid = part_bin_grid(ws.ntiles);
+template <bool SLOTS, int TB>
+hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                         uint16_t *slots, hipStream_t stream) {
+    const unsigned grid = part_bin_grid(ws.ntiles, TB);
     const bool cols = runs_as_columns(ws);
     uint32_t *runs = cols ? ws.run_starts : ws.run_rows;
     const int nb = (int)ws.nbins, ns = (int)ws.nsub, sh = (int)ws.sub_shift, g = (int)ws.group;
 #define BIN_LAUNCH(L, C)                                                                     \
-    k_part_bin<L, 0, SLOTS, C><<<grid, kPartBlock, 0, stream>>>(ks, mp, ws.pos, runs, nb, ns, sh, \
-                                                               g, ws.ntiles, slots)
+    do {                                                                                     \
+        k_part_bin<L, 0, SLOTS, C, TB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, nb,    \
+                                                                  ns, sh, g, ws.ntiles, slots); \
+    } while (0)
     if (ks.layout == KEYS_PACKED) {
         if (cols) BIN_LAUNCH(KEYS_PACKED, true); else BIN_LAUNCH(KEYS_PACKED, false);
     } else {
@@ -1057,6 +1066,16 @@ hipError_t launch_bin(const KeySpan &ks, const ModParams &mp, const PartitionWor
     return launch_runs_transpose(ws, stream);
 }
 
+// Pass 1 for a build (SLOTS = false) or a probe (SLOTS = true), then the
+// run-start transpose when the table is large.
+template <bool SLOTS>
+hipError_t launch_bin(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                      uint16_t *slots, hipStream_t stream) {
+    return tile_keys_of(ws) == 2 * kPartTileKeys
+               ? launch_bin_tb<SLOTS, 2 * kPartBlock>(ks, mp, ws, slots, stream)
+               : launch_bin_tb<SLOTS, kPartBlock>(ks, mp, ws, slots, stream);
+}
+
 hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                            hipStream_t stream) {
     if (ks.n == 0) return hipSuccess;
@@ -1065,12 +1084,13 @@ hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const Partiti
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
-template <int MODE, int G>
+template <int MODE, int G, int TP>
 hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                           uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                           hipStream_t stream) {
     static const bool attr_set = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<MODE, G>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(
+                                      &k_part_apply<MODE, G, 0, kApplyBlock, kApplyDepth, TP>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kSegMaxBits / 8));
         return true;
@@ -1078,23 +1098,45 @@ hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *wo
     (void)attr_set;
     const size_t lds = (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
     if (lds > kSegMaxBits / 8) return hipErrorInvalidValue;
-    k_part_apply<MODE, G><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
+    k_part_apply<MODE, G, 0, kApplyBlock, kApplyDepth, TP><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
         res, st);
     return hipGetLastError();
 }
 
+template <int MODE, int TP>
+hipError_t launch_apply_tp(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
+                           uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
+                           hipStream_t stream) {
+    switch (apply_lanes_per_tile(ws.nbins, TP)) {
+        case 2: return launch_apply_g<MODE, 2, TP>(ws, m, words, nw32, merge, res, st, stream);
+        case 4: return launch_apply_g<MODE, 4, TP>(ws, m, words, nw32, merge, res, st, stream);
+        case 8: return launch_apply_g<MODE, 8, TP>(ws, m, words, nw32, merge, res, st, stream);
+        case 16: return launch_apply_g<MODE, 16, TP>(ws, m, words, nw32, merge, res, st, stream);
+        case 32: return launch_apply_g<MODE, 32, TP>(ws, m, words, nw32, merge, res, st, stream);
+        default: return launch_apply_g<MODE, 64, TP>(ws, m, words, nw32, merge, res, st, stream);
+    }
+}
+
 template <int MODE>
 hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *words, uint64_t nw32,
                         int merge, uint8_t *res, const StackTable &st, hipStream_t stream) {
-    switch (apply_lanes_per_tile(ws.nbins)) {
-        case 2: return launch_apply_g<MODE, 2>(ws, m, words, nw32, merge, res, st, stream);
-        case 4: return launch_apply_g<MODE, 4>(ws, m, words, nw32, merge, res, st, stream);
-        case 8: return launch_apply_g<MODE, 8>(ws, m, words, nw32, merge, res, st, stream);
-        case 16: return launch_apply_g<MODE, 16>(ws, m, words, nw32, merge, res, st, stream);
-        case 32: return launch_apply_g<MODE, 32>(ws, m, words, nw32, merge, res, st, stream);
-        default: return launch_apply_g<MODE, 64>(ws, m, words, nw32, merge, res, st, stream);
-    }
+    return tile_keys_of(ws) == 2 * kPartTileKeys
+               ? launch_apply_tp<MODE, 2 * kPartTilePos>(ws, m, words, nw32, merge, res, st, stream)
+               : launch_apply_tp<MODE, kPartTilePos>(ws, m, words, nw32, merge, res, st, stream);
+}
+
+// The combine for the batch's tile size.
+hipError_t launch_combine(const PartitionWorkspace &ws, const uint8_t *res, const uint16_t *slots,
+                          size_t n, uint64_t *out, size_t nw, const StackTable &rows,
+                          hipStream_t stream) {
+    if (tile_keys_of(ws) == 2 * kPartTileKeys)
+        k_probe_combine<2 * (int)kPartTileKeys><<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(
+            res, slots, n, out, nw, rows);
+    else
+        k_probe_combine<(int)kPartTileKeys><<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(
+            res, slots, n, out, nw, rows);
+    return hipGetLastError();
 }
 
 hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const PartitionWorkspace &ws,
@@ -1117,9 +1159,7 @@ hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, cons
     if (e != hipSuccess) return e;
     StackTable rows{};
     rows.nf = 1;
-    k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out,
-                                                                       (ks.n + 63) / 64, rows);
-    return hipGetLastError();
+    return launch_combine(ws, res, slots, ks.n, out, (ks.n + 63) / 64, rows, stream);
 }
 
 hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, const StackTable &st,
@@ -1135,9 +1175,7 @@ hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, cons
     if (e != hipSuccess) return e;
     e = launch_apply<kApplyStack>(ws, mp_max.m, nullptr, 0, 0, res, st, stream);
     if (e != hipSuccess) return e;
-    k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(res, slots, ks.n, out, nw,
-                                                                       st);
-    return hipGetLastError();
+    return launch_combine(ws, res, slots, ks.n, out, nw, st, stream);
 }
 
 hipError_t launch_probe_lds(const KeySpan &ks, const ModParams &mp, const uint32_t *words,

@@ -274,7 +274,8 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
     uint64_t mmax = 0;
     PartitionWorkspace ws{};
     if (!ub_stack_plan(nf, ms, &mmax, &ws)) return -34;
-    ws.ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
+    ws.tile_keys = choose_tile_keys(ws.nbins);
+    ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
     ws.pos = pos;
     ws.run_rows = runs;
     ws.run_starts = runs + ws.ntiles * (ws.nbins + 1);
@@ -289,16 +290,21 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
     const size_t nw = (n + 63) / 64;
     const size_t lds = (size_t)ws.seg_bits / 8 * nf;
 #define UB_STACK(G, A, T) UB_STACKB(G, A, T, kApplyBlock)
-#define UB_STACKB(G, A, T, B)                                                                      \
+#define UB_STACKT(G, A, T, B, TP)                                                                  \
     do {                                                                                           \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<kApplyStack, G, A, B>), \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,                      \
-                                  (int)(kSegMaxBits / 8));                                         \
-        k_part_apply<kApplyStack, G, A, B><<<(unsigned)ws.nbins, B, lds, s>>>(                     \
+        (void)hipFuncSetAttribute(                                                                 \
+            reinterpret_cast<const void *>(&k_part_apply<kApplyStack, G, A, B, kApplyDepth, TP>),  \
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kSegMaxBits / 8));                   \
+        k_part_apply<kApplyStack, G, A, B, kApplyDepth, TP><<<(unsigned)ws.nbins, B, lds, s>>>(    \
             ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, mmax, nullptr, 0,   \
             0, res, T);                                                                            \
     } while (0)
-    const int G = apply_lanes_per_tile(ws.nbins);
+#define UB_STACKB(G, A, T, B)                                                                      \
+    do {                                                                                           \
+        if (ws.tile_keys == 2 * kPartTileKeys) UB_STACKT(G, A, T, B, 2 * kPartTilePos);            \
+        else UB_STACKT(G, A, T, B, kPartTilePos);                                                  \
+    } while (0)
+    const int G = apply_lanes_per_tile(ws.nbins, 3 * tile_keys_of(ws));
     StackTable one = st;
     one.nf = 1;
     switch (variant) {
@@ -312,7 +318,7 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
             if (G == 4) UB_STACK(4, 0, one); else if (G == 8) UB_STACK(8, 0, one); else return -22;
             break;
         case 5:
-            k_probe_combine<<<(unsigned)ws.ntiles, kCombineBlock, 0, s>>>(res, slots, n, out, nw, st);
+            return launch_combine(ws, res, slots, n, out, nw, st, s) == hipSuccess ? 0 : -5;
             break;
         case 6:
             if (G == 4) UB_STACK(4, 3, st); else if (G == 8) UB_STACK(8, 3, st); else return -22;
@@ -331,5 +337,6 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
     }
 #undef UB_STACK
 #undef UB_STACKB
+#undef UB_STACKT
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
