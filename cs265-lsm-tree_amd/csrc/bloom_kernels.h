@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "bloom_math.h"
 
@@ -111,8 +112,13 @@ struct PartitionWorkspace {
 // (> 1024 segments: under 12 entries per segment and 4096-key tile) make
 // pass 2 line-bound, so such batches sort 8192-key tiles (one 1024-thread
 // workgroup per CU) and get runs twice as long (tools/ubench.py part_c4).
+// BLOOMHIP_BIG_TILE_BINS overrides the 1024 threshold (tuning experiments).
 inline uint32_t choose_tile_keys(size_t nbins) {
-    return nbins > 1024 ? 2 * (uint32_t)kPartTileKeys : (uint32_t)kPartTileKeys;
+    static const size_t threshold = [] {
+        const char *e = getenv("BLOOMHIP_BIG_TILE_BINS");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)512;
+    }();
+    return nbins > threshold ? 2 * (uint32_t)kPartTileKeys : (uint32_t)kPartTileKeys;
 }
 inline size_t tile_keys_of(const PartitionWorkspace &ws) {
     return ws.tile_keys ? ws.tile_keys : kPartTileKeys;

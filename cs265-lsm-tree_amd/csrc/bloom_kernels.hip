@@ -20,6 +20,8 @@
 //               the segment out with coalesced stores.  No global atomics.
 #include "bloom_kernels.h"
 
+#include <stdlib.h>
+
 namespace bloomhip {
 
 namespace {
@@ -730,33 +732,51 @@ __global__ void __launch_bounds__(kProbeLdsBlock) k_probe_lds(KeySpan ks, const 
 // tile stages the tile's result bytes (sorted order) in LDS and, for each key,
 // ANDs the bytes at its three slots; bit j of the AND is filter j's is_set,
 // packed 64 keys per u64 by a 64-lane ballot into row rows.row[j] of out.
-constexpr int kCombineBlock = 256;
+// Each thread owns TILE_KEYS / kCombineBlock keys (lane-consecutive per
+// wave, for the ballot) and issues all of their slot loads before it waits on
+// anything, so a workgroup pays one memory latency, not one per key step.
+// Lane j < nf stores member j's word of each 64-key step.
+constexpr int kCombineBlock = 1024;
 
 template <int TILE_KEYS>
 __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, size_t n,
     uint64_t *__restrict__ out, size_t nw, StackTable rows) {
     constexpr int kTilePos = 3 * TILE_KEYS;
+    constexpr int kPer = TILE_KEYS / kCombineBlock;
+    static_assert(kPer * kCombineBlock == TILE_KEYS, "whole key steps");
     __shared__ __attribute__((aligned(16))) uint8_t s_r[kTilePos];
     const size_t tile = blockIdx.x;
     const size_t tile0 = tile * TILE_KEYS;
     const int tile_keys = (int)min((size_t)TILE_KEYS, n - tile0);
+    const uint16_t *sl = slots + tile * 3 * TILE_KEYS;
+    uint32_t sa[kPer], sb[kPer], sc[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        const int key = j * kCombineBlock + (int)threadIdx.x;
+        const bool live = key < tile_keys;
+        sa[j] = live ? sl[key] : 0u;
+        sb[j] = live ? sl[TILE_KEYS + key] : 0u;
+        sc[j] = live ? sl[2 * TILE_KEYS + key] : 0u;
+    }
     const uint4 *src = reinterpret_cast<const uint4 *>(res + tile * (size_t)kTilePos);
     for (int q = threadIdx.x; q < kTilePos / 16; q += kCombineBlock)
         reinterpret_cast<uint4 *>(s_r)[q] = src[q];
     __syncthreads();
-    const uint16_t *sl = slots + tile * 3 * TILE_KEYS;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int j = 0; j < (int)TILE_KEYS / kCombineBlock; j++) {
+    const int nf = rows.nf;
+    const int my_row = lane < nf ? rows.row[lane] : 0;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
         const int key = j * kCombineBlock + (int)threadIdx.x;
-        uint32_t hit = 0;
-        if (key < tile_keys)
-            hit = s_r[sl[key]] & s_r[sl[TILE_KEYS + key]] & s_r[sl[2 * TILE_KEYS + key]];
+        const uint32_t hit = key < tile_keys ? (uint32_t)(s_r[sa[j]] & s_r[sb[j]] & s_r[sc[j]]) : 0u;
         const int base = j * kCombineBlock + wave * 64;
-        for (int f = 0; f < rows.nf; f++) {
+        uint64_t mine = 0;
+        for (int f = 0; f < nf; f++) {
             const uint64_t ballot = __ballot((hit >> f) & 1u);
-            if (lane == 0 && base < tile_keys) out[(size_t)rows.row[f] * nw + (tile0 + base) / 64] = ballot;
+            if (lane == f) mine = ballot;
         }
+        if (lane < nf && base < tile_keys) out[(size_t)my_row * nw + (tile0 + base) / 64] = mine;
     }
 }
 
@@ -800,6 +820,25 @@ __global__ void __launch_bounds__(kMetaBlock) k_run_meta(KeySpan ks, int32_t *__
 
 constexpr int kRouteBlock = 256;
 
+// this lane's value becomes `r` where bit `lane` of the wave mask is set
+__device__ __forceinline__ int32_t select_by_mask(uint64_t mask, int32_t r, int32_t v) {
+    int32_t out;
+    asm volatile("v_cndmask_b32 %0, %1, %2, %3" : "=v"(out) : "v"(v), "v"(r), "s"(mask));
+    return out;
+}
+
+// One wave handles 64 consecutive keys per step, fetched one step ahead with
+// the step's candidate words (lane r < nruns loads run r's word; the
+// range-checked words leave the same way, one store per run from lane r).
+// Per run the candidate test is wave-mask work: the filter word (read from
+// lane r) AND the ballot of the range check; the newest candidate run is
+// picked with a mask select.  Page search (upper_bound over the run's
+// fences, staged in LDS): one interpolation guess from the run's first and
+// last fence, a bracket of +-kRouteWindow fences around it, and a binary
+// search inside the bracket (or over the whole range when the guess missed:
+// exact either way, only slower).
+constexpr int kRouteWindow = 8;
+
 template <int LAYOUT, bool LDS_FENCES>
 __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
                                                       uint64_t *__restrict__ cand, size_t nw,
@@ -807,76 +846,106 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
                                                       int32_t *__restrict__ page) {
     extern __shared__ int32_t s_fences[];
     __shared__ int32_t s_lo[kMaxRouteRuns], s_hi[kMaxRouteRuns];
-    for (int r = threadIdx.x; r < t.nruns; r += kRouteBlock) {
-        s_hi[r] = t.meta[r][0];
-        s_lo[r] = t.nfences[r] ? t.meta[r][1] : 0;
+    __shared__ uint32_t s_nf[kMaxRouteRuns], s_off[kMaxRouteRuns];
+    __shared__ float s_scale[kMaxRouteRuns];
+    const int nruns = t.nruns;
+    for (int r = threadIdx.x; r < nruns; r += kRouteBlock) {
+        const uint32_t nf = t.nfences[r];
+        const int32_t f0 = nf ? t.meta[r][1] : 0, fl = nf ? t.meta[r][nf] : 0;
+        s_hi[r] = nf ? t.meta[r][0] : INT32_MIN;  // no fences: never in range
+        s_lo[r] = nf ? f0 : INT32_MAX;
+        s_nf[r] = nf;
+        s_off[r] = t.fence_off[r];
+        s_scale[r] = (nf > 1 && fl > f0) ? (float)(nf - 1) / ((float)fl - (float)f0) : 0.0f;
     }
     if constexpr (LDS_FENCES) {
-        for (int r = 0; r < t.nruns; r++)
-            for (uint32_t i = threadIdx.x; i < t.nfences[r]; i += kRouteBlock)
-                s_fences[t.fence_off[r] + i] = t.meta[r][1 + i];
-    }
-    __syncthreads();
-    auto fence = [&](int r, uint32_t i) -> int32_t {
-        if constexpr (LDS_FENCES) return s_fences[t.fence_off[r] + i];
-        else return t.meta[r][1 + i];
-    };
-    const int lane = threadIdx.x & 63;
-    for (size_t w = ((size_t)blockIdx.x * kRouteBlock + threadIdx.x) >> 6; w < nw;
-         w += ((size_t)gridDim.x * kRouteBlock) >> 6) {
-        const size_t i = w * 64 + lane;
-        const bool valid = i < ks.n;
-        int32_t k = 0;
-        if (valid) {
-            if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
-            else k = load_key(ks, i);
-        }
-        int32_t fr = -1;
-        for (int r = 0; r < t.nruns; r++) {
-            const uint64_t bits = cand[(size_t)r * nw + w];
-            const bool c = valid && ((bits >> lane) & 1u) && t.nfences[r] > 0 &&
-                           k >= s_lo[r] && k <= s_hi[r];
-            const uint64_t b = __ballot(c);
-            if (lane == 0) cand[(size_t)r * nw + w] = b;
-            if (c && fr < 0) fr = r;
-        }
-        int32_t pg = -1;
-        if (fr >= 0) {
-            // upper_bound(fences, k).  A run's keys are sorted and, in an LSM,
-            // close to uniform, so interpolation steps narrow the range in
-            // few LDS reads; a binary search finishes (and bounds the worst
-            // case).  Invariant: fences [0, lo) are <= k, [hi, n) are > k.
-            const uint32_t n = t.nfences[fr];
-            uint32_t lo = 0, hi = n;
-            if (n > 16) {
-                int32_t a = fence(fr, 0), z = fence(fr, n - 1);
-                if (k < a) {
-                    hi = 0;
-                } else if (k >= z) {
-                    lo = n;
-                } else {  // a <= k < z: the answer is in [1, n - 1]
-                    lo = 1;
-                    hi = n - 1;
-                    for (int it = 0; it < 3 && hi - lo > 8; it++) {
-                        // a = a fence <= k just below lo, z = a fence > k at/after hi
-                        const float frac = (float)((double)k - a) / (float)((double)z - a);
-                        uint32_t g = lo + (uint32_t)(frac * (float)(hi - lo));
-                        g = min(max(g, lo), hi - 1);
-                        const int32_t fg = fence(fr, g);
-                        if (fg <= k) {
-                            lo = g + 1;
-                            a = fg;
-                        } else {
-                            hi = g;
-                            z = fg;
-                        }
-                    }
+        // eight independent loads in flight per thread per batch
+        constexpr int kBatch = 8;
+        for (int r = 0; r < nruns; r++) {
+            const uint32_t nf = t.nfences[r];
+            const int32_t *src = t.meta[r] + 1;
+            int32_t *dst = s_fences + t.fence_off[r];
+            for (uint32_t b = 0; b < nf; b += kBatch * kRouteBlock) {
+                int32_t v[kBatch];
+#pragma unroll
+                for (int q = 0; q < kBatch; q++) {
+                    const uint32_t i = b + q * kRouteBlock + threadIdx.x;
+                    v[q] = i < nf ? src[i] : 0;
+                }
+#pragma unroll
+                for (int q = 0; q < kBatch; q++) {
+                    const uint32_t i = b + q * kRouteBlock + threadIdx.x;
+                    if (i < nf) dst[i] = v[q];
                 }
             }
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (fence(fr, mid) <= k) lo = mid + 1;
-                else hi = mid;
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const size_t wstep = ((size_t)gridDim.x * kRouteBlock) >> 6;
+    size_t w = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(((size_t)blockIdx.x * kRouteBlock + threadIdx.x) >> 6));
+    // Unconditional (clamped) loads: a load under a branch makes the
+    // compiler's wait counting fall back to waiting for everything.
+    auto load_key_at = [&](size_t ww) -> int32_t {
+        const size_t i = min(min(ww, nw - 1) * 64 + lane, ks.n - 1);  // ks.n >= 1 here
+        if constexpr (LAYOUT == KEYS_PACKED) return reinterpret_cast<const int32_t *>(ks.base)[i];
+        else return load_key(ks, i);
+    };
+    auto load_cand_at = [&](size_t ww) -> uint64_t {
+        return cand[(size_t)min(lane, nruns - 1) * nw + min(ww, nw - 1)];
+    };
+    // One step of 64 keys.  The loop below runs two steps per iteration on
+    // two register sets, each set's loads issued a whole step ahead (a
+    // single loop-carried set made the compiler wait for the prefetch
+    // right away, at the copy).
+    auto step = [&](size_t w, int32_t k, uint64_t cw) {
+        const size_t i = w * 64 + lane;
+        const bool valid = i < ks.n;
+        int32_t fr = -1;
+        uint64_t newc = 0, open = ~0ull;  // open: lanes without a candidate run yet
+        for (int r = 0; r < nruns; r++) {
+            // (readlane returns int: through uint32_t, or the low half sign-extends)
+            const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cw, r);
+            const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cw >> 32), r);
+            const uint64_t b = (((uint64_t)bhi << 32) | blo) &
+                               __ballot(valid && k >= s_lo[r] && k <= s_hi[r]);
+            if (lane == r) newc = b;
+            fr = select_by_mask(b & open, r, fr);
+            open &= ~b;
+        }
+        if (lane < nruns) cand[(size_t)lane * nw + w] = newc;
+        int32_t pg = -1;
+        if (fr >= 0) {
+            // upper_bound(fences, k); k >= fences[0] (range check), so the
+            // answer is in [1, n].  Invariant: [0, lo) <= k, [hi, n) > k.
+            const uint32_t n = s_nf[fr];
+            uint32_t lo = 1, hi = n;
+            if constexpr (LDS_FENCES) {
+                const int32_t *fz = s_fences + s_off[fr];
+                if (n > 2 * kRouteWindow) {
+                    const float gf = ((float)k - (float)s_lo[fr]) * s_scale[fr];
+                    const int g = min((int)max(gf, 0.0f), (int)n - 1);
+                    const int a = max(g - kRouteWindow, 1), z = min(g + kRouteWindow, (int)n - 1);
+                    const int32_t fa = fz[a], fzz = fz[z];
+                    if (fa <= k) lo = a + 1; else hi = a;
+                    if (fzz > k) hi = min(hi, (uint32_t)z); else lo = max(lo, (uint32_t)z + 1);
+                }
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (fz[mid] <= k) lo = mid + 1;
+                    else hi = mid;
+                }
+            } else {
+                // fences beyond the LDS budget: binary search in global memory
+                const int32_t *fz = t.meta[0];
+                for (int r = 0; r < nruns; r++)  // this lane's run (kernarg pointers)
+                    if (r == fr) fz = t.meta[r] + 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (fz[mid] <= k) lo = mid + 1;
+                    else hi = mid;
+                }
             }
             pg = (int32_t)lo - 1;
         }
@@ -884,6 +953,19 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
             if (first) first[i] = fr;
             if (page) page[i] = pg;
         }
+    };
+    int32_t ka = load_key_at(w);
+    uint64_t ca = load_cand_at(w);
+    while (w < nw) {
+        const int32_t kb = load_key_at(w + wstep);
+        const uint64_t cb = load_cand_at(w + wstep);
+        step(w, ka, ca);
+        w += wstep;
+        if (w >= nw) break;
+        ka = load_key_at(w + wstep);
+        ca = load_cand_at(w + wstep);
+        step(w, kb, cb);
+        w += wstep;
     }
 }
 
@@ -1222,11 +1304,15 @@ hipError_t launch_route(const KeySpan &ks, const RouteTable &t, uint64_t *cand, 
                         int32_t *first, int32_t *page, hipStream_t stream) {
     if (nw == 0) return hipSuccess;
     const size_t lds = (size_t)t.total_fences * 4;
-    // Fences from LDS beat L2 reads (C3: 0.24 vs 0.35 ms), even though every
-    // workgroup stages all of them; capping the grid to amortise the staging
-    // lost more to latency than it saved (0.28 ms).
+    // Fences from LDS beat L2 reads.  The grid is what fits on the chip at
+    // once (the staged fences bound the workgroups per CU), and every wave
+    // walks many 64-key steps, so each workgroup stages the fences once.
     const bool in_lds = lds <= kRouteLdsFenceBytes;
-    const unsigned grid = grid_for(nw, kRouteBlock / 64, 16384u);
+    const size_t per_block = (in_lds ? lds : 0) + 2048;
+    int per_cu = (int)(kLdsBitmapBytes / per_block);
+    per_cu = per_cu < 1 ? 1 : per_cu > 8 ? 8 : per_cu;  // 8 x 256 threads = 32 waves per CU
+    if (const char *e = getenv("BLOOMHIP_ROUTE_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
+    const unsigned grid = grid_for(nw, kRouteBlock / 64, (unsigned)(device_cu_count() * per_cu));
 #define ROUTE_LAUNCH(L, F) \
     k_route<L, F><<<grid, kRouteBlock, F ? lds : 0, stream>>>(ks, t, cand, nw, first, page)
     if (ks.layout == KEYS_PACKED) {
