@@ -688,16 +688,17 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
         for (size_t b = a + 1; b < cand.size() && mem.size() < (size_t)kMaxStack; b++)
             if (!done[cand[b]] && mh % filters[cand[b]]->m == 0) mem.push_back(cand[b]);
         bool explicit_stack = false;
-        uint64_t g = 0;
+        uint64_t g = 0, mmin = ~0ull;
         double alone = 0;
         for (int j : mem) {
+            mmin = std::min(mmin, filters[j]->m);
             explicit_stack |= effective_probe_strategy(filters[j], f0->probe_strategy) ==
                               BLOOMHIP_PROBE_STACKED;
             g = std::gcd(g, filters[j]->m);
             alone += probe_cost_alone(filters[j], n);
         }
         PartitionWorkspace ws{};
-        if (!plan_stack(mh, g, (int)mem.size(), ncu, &ws)) continue;
+        if (!plan_stack(mh, g, mmin, (int)mem.size(), ncu, &ws)) continue;
         if (!explicit_stack && (mem.size() < 2 || n < kProbePartitionMinKeys ||
                                 ws.nbins < (size_t)ncu || alone <= kCostStacked))
             continue;
@@ -705,7 +706,7 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
         st.nf = (int)mem.size();
         for (int k = 0; k < st.nf; k++) {
             st.words[k] = filters[mem[k]]->d_words;
-            st.nseg[k] = (uint32_t)(filters[mem[k]]->m / ws.seg_bits);
+            st.mwords[k] = (uint32_t)(filters[mem[k]]->m / 32);
             st.row[k] = mem[k];
         }
         Workspace *w = workspace_for(f0->device, s);

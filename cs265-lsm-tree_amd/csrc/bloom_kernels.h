@@ -61,6 +61,8 @@ constexpr size_t kLdsBitmapBytes = 160 * 1024;
 // of segments is a multiple of the CU count: every CU of pass 2 gets the same
 // share.
 constexpr uint32_t kSegMaxBits = 144u * 1024u * 8u;  // 144 KiB of LDS
+// A stacked probe's pass 2 has no static LDS: its images may use all 160 KiB.
+constexpr uint32_t kStackMaxBits = 160u * 1024u * 8u;
 constexpr int kPartBlock = 512;
 constexpr int kPartKPT = 8;  // keys per thread in pass 1
 constexpr size_t kPartTileKeys = (size_t)kPartBlock * kPartKPT;  // 4096
@@ -90,7 +92,7 @@ constexpr int kMaxStack = 8;
 
 struct StackTable {
     const uint32_t *words[kMaxStack];  // member bitmaps (32-bit word view)
-    uint32_t nseg[kMaxStack];          // m_j / w: member j's segment count
+    uint32_t mwords[kMaxStack];        // m_j / 32: member j's size in words (m_j % 128 == 0)
     int row[kMaxStack];                // output row of member j
     int nf;
 };
@@ -125,9 +127,12 @@ inline size_t tile_keys_of(const PartitionWorkspace &ws) {
 }
 
 // Geometry of a stacked probe (seg_bits = w): false when no w = g << s with
-// w | gcd_m, nf * w bits <= kSegMaxBits and <= kPartMaxBins sub-segments
-// exists.  Prefers the widest w that still gives >= ncu segments.
-bool plan_stack(uint64_t m_max, uint64_t gcd_m, int nf, int ncu, PartitionWorkspace *ws);
+// w | m_max, w <= m_min (the smallest member), nf * w bits <= kStackMaxBits
+// and <= kPartMaxBins sub-segments exists.  Prefers the widest w that still
+// gives >= ncu segments.  gcd_m: gcd of the members' sizes (a multiple of
+// 128 bits).
+bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
+                PartitionWorkspace *ws);
 
 // CUs of the current device (cached).
 int device_cu_count();

@@ -372,7 +372,14 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
 // go through the transpose: at C4 (805 MB) the column stores cost ~2.1 ms
 // (partial-line write-backs), the transpose 0.39 ms (tools/ubench.py part*).
 // ---------------------------------------------------------------------------
-constexpr size_t kColumnTableMaxBytes = 16u << 20;
+// BLOOMHIP_COLUMN_TABLE_MAX (bytes) overrides the 16 MiB limit (tuning).
+static size_t column_table_max_bytes() {
+    static const size_t v = [] {
+        const char *e = getenv("BLOOMHIP_COLUMN_TABLE_MAX");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(16u << 20);
+    }();
+    return v;
+}
 constexpr int kTransposeTile = 64;
 constexpr int kTransposeBlock = 256;
 
@@ -420,7 +427,7 @@ inline int apply_lanes_per_tile(size_t nbins, size_t tile_pos = kPartTilePos) {
 // segment.  kApplyProbe: the LDS image is the filter's segment; each entry's
 // bit is written as one result byte at the entry's own index in the sorted
 // tile (res[tile*kPartTilePos + index]), so the result stores follow the runs
-// like the loads.  kApplyStack: LDS holds segment b % nseg[j] of every stack
+// like the loads.  kApplyStack: LDS holds bits [b*w, (b+1)*w) mod m_j of every stack
 // member j (StackTable), the result byte carries member j's bit at bit j.
 // (Writing the results over the positions instead, 4 B each, made the whole
 // probe slower: the combine then reads 4x the bytes; tools/ubench.py stack.)
@@ -467,13 +474,19 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const uint32_t base = (uint32_t)b * seg_bits;             // entries are full positions
     const uint32_t lim = (uint32_t)min((uint64_t)seg_bits, m - base);
     if constexpr (MODE == kApplyStack) {
-        // member j's segment b % nseg[j]: seg_words is a multiple of 4 and
-        // every member is a whole number of segments (plan_stack)
+        // member j's bits (b*w + o) mod m_j for o < w: the w bits from
+        // (b*w) mod m_j on, wrapping at m_j (w <= m_j; w and m_j are
+        // multiples of 128 bits, so no 16-B vector straddles the wrap)
         for (int j = 0; j < st.nf; j++) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(
-                st.words[j] + (size_t)((uint32_t)b % st.nseg[j]) * seg_words);
+            const uint32_t mw = st.mwords[j];
+            const uint32_t start = (uint32_t)(((uint64_t)b * seg_words) % mw);
+            const uint4 *src = reinterpret_cast<const uint4 *>(st.words[j]);
             uint4 *dst = reinterpret_cast<uint4 *>(seg + (size_t)j * seg_words);
-            for (int i = threadIdx.x; i < (int)seg_words / 4; i += BLOCK) dst[i] = src[i];
+            for (int i = threadIdx.x; i < (int)seg_words / 4; i += BLOCK) {
+                uint32_t wi = start + 4u * (uint32_t)i;
+                if (wi >= mw) wi -= mw;
+                dst[i] = src[wi / 4];
+            }
         }
     } else if constexpr (MODE == kApplyProbe) {
         for (int i = threadIdx.x; i < (int)seg_words; i += BLOCK)
@@ -736,9 +749,8 @@ __global__ void __launch_bounds__(kProbeLdsBlock) k_probe_lds(KeySpan ks, const 
 // wave, for the ballot) and issues all of their slot loads before it waits on
 // anything, so a workgroup pays one memory latency, not one per key step.
 // Lane j < nf stores member j's word of each 64-key step.
-constexpr int kCombineBlock = 1024;
-
-template <int TILE_KEYS>
+constexpr int kCombineBlockDefault = 1024;  // 1024: 42 us at C3, 512: 45, 256: 53
+template <int TILE_KEYS, int kCombineBlock>
 __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, size_t n,
     uint64_t *__restrict__ out, size_t nw, StackTable rows) {
@@ -832,14 +844,17 @@ __device__ __forceinline__ int32_t select_by_mask(uint64_t mask, int32_t r, int3
 // range-checked words leave the same way, one store per run from lane r).
 // Per run the candidate test is wave-mask work: the filter word (read from
 // lane r) AND the ballot of the range check; the newest candidate run is
-// picked with a mask select.  Page search (upper_bound over the run's
-// fences, staged in LDS): one interpolation guess from the run's first and
-// last fence, a bracket of +-kRouteWindow fences around it, and a binary
-// search inside the bracket (or over the whole range when the guess missed:
-// exact either way, only slower).
-constexpr int kRouteWindow = 8;
+// picked with a mask select.  NR > 0 fixes the run count at compile time (the
+// run loop unrolls; the kernel is instruction-issue bound, PMC: ~160 VALU +
+// ~125 SALU per step before).  Page search (upper_bound over the run's fences,
+// staged in LDS): one interpolation guess from the run's first and last
+// fence places a window of kRouteWindow fences; two reads check that the
+// answer lies in it, and a branchless 4-step search finds it there.  When
+// the check fails, a binary search over the whole run does (exact either
+// way, only slower).
+constexpr int kRouteWindow = 15;  // fences; answers a .. a + 15: 4 halving steps
 
-template <int LAYOUT, bool LDS_FENCES>
+template <int LAYOUT, bool LDS_FENCES, int NR>
 __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
                                                       uint64_t *__restrict__ cand, size_t nw,
                                                       int32_t *__restrict__ first,
@@ -848,7 +863,7 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
     __shared__ int32_t s_lo[kMaxRouteRuns], s_hi[kMaxRouteRuns];
     __shared__ uint32_t s_nf[kMaxRouteRuns], s_off[kMaxRouteRuns];
     __shared__ float s_scale[kMaxRouteRuns];
-    const int nruns = t.nruns;
+    const int nruns = NR > 0 ? NR : t.nruns;
     for (int r = threadIdx.x; r < nruns; r += kRouteBlock) {
         const uint32_t nf = t.nfences[r];
         const int32_t f0 = nf ? t.meta[r][1] : 0, fl = nf ? t.meta[r][nf] : 0;
@@ -904,7 +919,9 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
         const bool valid = i < ks.n;
         int32_t fr = -1;
         uint64_t newc = 0, open = ~0ull;  // open: lanes without a candidate run yet
-        for (int r = 0; r < nruns; r++) {
+#pragma unroll
+        for (int r = 0; r < (NR > 0 ? NR : kMaxRouteRuns); r++) {
+            if (NR == 0 && r >= nruns) break;
             // (readlane returns int: through uint32_t, or the low half sign-extends)
             const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cw, r);
             const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cw >> 32), r);
@@ -918,36 +935,52 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
         int32_t pg = -1;
         if (fr >= 0) {
             // upper_bound(fences, k); k >= fences[0] (range check), so the
-            // answer is in [1, n].  Invariant: [0, lo) <= k, [hi, n) > k.
-            const uint32_t n = s_nf[fr];
-            uint32_t lo = 1, hi = n;
+            // answer is in [1, n].
+            const int n = (int)s_nf[fr];
+            int lo;
+            bool ok = true;
             if constexpr (LDS_FENCES) {
                 const int32_t *fz = s_fences + s_off[fr];
-                if (n > 2 * kRouteWindow) {
+                int a = 0;
+                if (n > kRouteWindow) {
                     const float gf = ((float)k - (float)s_lo[fr]) * s_scale[fr];
-                    const int g = min((int)max(gf, 0.0f), (int)n - 1);
-                    const int a = max(g - kRouteWindow, 1), z = min(g + kRouteWindow, (int)n - 1);
-                    const int32_t fa = fz[a], fzz = fz[z];
-                    if (fa <= k) lo = a + 1; else hi = a;
-                    if (fzz > k) hi = min(hi, (uint32_t)z); else lo = max(lo, (uint32_t)z + 1);
+                    const int g = (int)max(gf, 0.0f);
+                    a = min(max(g - kRouteWindow / 2, 0), n - kRouteWindow);
+                    // the answer is in [a, a + 15] iff fences[a - 1] <= k and
+                    // fences[a + 15] > k (a window at either end passes that side)
+                    const int32_t fl = fz[max(a - 1, 0)], fh = fz[min(a + kRouteWindow, n - 1)];
+                    ok = (a == 0 || fl <= k) && (a + kRouteWindow >= n || fh > k);
                 }
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (fz[mid] <= k) lo = mid + 1;
-                    else hi = mid;
+                lo = a;
+#pragma unroll
+                for (int st = 8; st >= 1; st >>= 1) {  // fences at index >= n count as > k
+                    const int idx = lo + st - 1;
+                    if (idx < n && fz[min(idx, n - 1)] <= k) lo += st;
+                }
+                if (!ok) {  // the guess missed (rare): binary search the whole run
+                    int l = 1, h = n;
+                    while (l < h) {
+                        const int mid = (l + h) >> 1;
+                        if (fz[mid] <= k) l = mid + 1;
+                        else h = mid;
+                    }
+                    lo = l;
                 }
             } else {
                 // fences beyond the LDS budget: binary search in global memory
                 const int32_t *fz = t.meta[0];
                 for (int r = 0; r < nruns; r++)  // this lane's run (kernarg pointers)
                     if (r == fr) fz = t.meta[r] + 1;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (fz[mid] <= k) lo = mid + 1;
-                    else hi = mid;
+                int l = 1, h = n;
+                while (l < h) {
+                    const int mid = (l + h) >> 1;
+                    if (fz[mid] <= k) l = mid + 1;
+                    else h = mid;
                 }
+                lo = l;
             }
-            pg = (int32_t)lo - 1;
+            (void)ok;
+            pg = lo - 1;
         }
         if (valid) {
             if (first) first[i] = fr;
@@ -1071,15 +1104,27 @@ bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
     return true;
 }
 
-bool plan_stack(uint64_t m_max, uint64_t gcd_m, int nf, int ncu, PartitionWorkspace *ws) {
+bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
+                PartitionWorkspace *ws) {
     if (m_max == 0 || m_max > 0xFFFFFFFFull || nf < 1 || nf > kMaxStack || gcd_m == 0 ||
-        m_max % gcd_m != 0)
+        m_max % gcd_m != 0 || gcd_m % 128 != 0 || m_min < gcd_m)
         return false;
-    const uint64_t wmax = kSegMaxBits / (uint64_t)nf;  // every member's w bits in LDS
+    // Segment widths w: w | gcd_m, so every member is a whole number of
+    // segments, in at most 144 KiB of images (two pass-2 workgroups per CU
+    // when they fit in 80 KiB).  BLOOMHIP_STACK_WRAP=1 (tuning experiments)
+    // asks only w | m_max and w <= m_min, in up to 160 KiB: the staging reads
+    // each member from (b*w) mod m_j with wraparound.  At C3 that doubles w
+    // (640 segments instead of 1280, one workgroup per CU) and was no faster:
+    // pass 1 121 vs 129 us, pass 2 163 vs 153 us (profiles/r01/s3/).
+    static const bool wrap = [] {
+        const char *e = getenv("BLOOMHIP_STACK_WRAP");
+        return e && e[0] == '1';
+    }();
+    const uint64_t divisor = wrap ? m_max : gcd_m;
+    const uint64_t wmax = (wrap ? kStackMaxBits : kSegMaxBits) / (uint64_t)nf;
     uint32_t s0 = 5;
     while ((((m_max - 1) >> s0) + 1) > kPartMaxBins) s0++;
-    // candidates w = g << s dividing gcd_m (so every member, and m_max, is a
-    // whole number of segments), 128-bit multiples for the 16-B image loads
+    // candidates w = g << s, 128-bit multiples for the 16-B image loads
     uint64_t best_w = 0;
     uint32_t best_s = 0;
     // The segment count sets the run length per tile (kPartTilePos / nbins),
@@ -1092,10 +1137,10 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, int nf, int ncu, PartitionWorksp
         return a ? w > best_w : w < best_w;
     };
     for (uint32_t s = s0; s < 32 && (1ull << s) <= wmax; s++) {
-        if (gcd_m % (1ull << s)) break;  // larger s cannot divide either
+        if (divisor % (1ull << s)) break;  // larger s cannot divide either
         for (uint64_t g = wmax >> s; g >= 1; g--) {
             const uint64_t w = g << s;
-            if (w % 128 || gcd_m % w) continue;
+            if (w % 128 || divisor % w || w > m_min) continue;
             if (better(w) || (w == best_w && s > best_s)) {
                 best_w = w;
                 best_s = s;
@@ -1122,7 +1167,7 @@ hipError_t launch_runs_transpose(const PartitionWorkspace &ws, hipStream_t strea
 }
 
 bool runs_as_columns(const PartitionWorkspace &ws) {
-    return ws.ntiles * (ws.nbins + 1) * 4 <= kColumnTableMaxBytes;
+    return ws.ntiles * (ws.nbins + 1) * 4 <= column_table_max_bytes();
 }
 
 template <bool SLOTS, int TB>
@@ -1174,12 +1219,12 @@ hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *wo
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(
                                       &k_part_apply<MODE, G, 0, kApplyBlock, kApplyDepth, TP>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)(kSegMaxBits / 8));
+                                  (int)((MODE == kApplyStack ? kStackMaxBits : kSegMaxBits) / 8));
         return true;
     }();
     (void)attr_set;
     const size_t lds = (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
-    if (lds > kSegMaxBits / 8) return hipErrorInvalidValue;
+    if (lds > (MODE == kApplyStack ? kStackMaxBits : kSegMaxBits) / 8) return hipErrorInvalidValue;
     k_part_apply<MODE, G, 0, kApplyBlock, kApplyDepth, TP><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
         res, st);
@@ -1212,12 +1257,27 @@ hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *word
 hipError_t launch_combine(const PartitionWorkspace &ws, const uint8_t *res, const uint16_t *slots,
                           size_t n, uint64_t *out, size_t nw, const StackTable &rows,
                           hipStream_t stream) {
-    if (tile_keys_of(ws) == 2 * kPartTileKeys)
-        k_probe_combine<2 * (int)kPartTileKeys><<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(
-            res, slots, n, out, nw, rows);
-    else
-        k_probe_combine<(int)kPartTileKeys><<<(unsigned)ws.ntiles, kCombineBlock, 0, stream>>>(
-            res, slots, n, out, nw, rows);
+    // workgroup size: BLOOMHIP_COMBINE_BLOCK (256 / 512 / 1024) for tuning
+    static const int cb = [] {
+        const char *e = getenv("BLOOMHIP_COMBINE_BLOCK");
+        const int v = e ? atoi(e) : kCombineBlockDefault;
+        return (v == 256 || v == 512 || v == 1024) ? v : kCombineBlockDefault;
+    }();
+#define COMBINE(TK, CB) \
+    k_probe_combine<TK, CB><<<(unsigned)ws.ntiles, CB, 0, stream>>>(res, slots, n, out, nw, rows)
+#define COMBINE_CB(TK)                           \
+    switch (cb) {                                \
+        case 256: COMBINE(TK, 256); break;       \
+        case 512: COMBINE(TK, 512); break;       \
+        default: COMBINE(TK, 1024); break;       \
+    }
+    if (tile_keys_of(ws) == 2 * kPartTileKeys) {
+        COMBINE_CB(2 * (int)kPartTileKeys)
+    } else {
+        COMBINE_CB((int)kPartTileKeys)
+    }
+#undef COMBINE_CB
+#undef COMBINE
     return hipGetLastError();
 }
 
@@ -1252,7 +1312,9 @@ hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, cons
         (uint64_t)ws.nbins * ws.seg_bits != mp_max.m)
         return hipErrorInvalidValue;
     for (int j = 0; j < st.nf; j++)
-        if (st.nseg[j] == 0 || ws.nbins % st.nseg[j] != 0) return hipErrorInvalidValue;
+        if (st.mwords[j] % 4 != 0 || (uint64_t)st.mwords[j] * 32 < ws.seg_bits ||
+            mp_max.m % ((uint64_t)st.mwords[j] * 32) != 0)
+            return hipErrorInvalidValue;
     hipError_t e = launch_bin<true>(ks, mp_max, ws, slots, stream);
     if (e != hipSuccess) return e;
     e = launch_apply<kApplyStack>(ws, mp_max.m, nullptr, 0, 0, res, st, stream);
@@ -1313,13 +1375,26 @@ hipError_t launch_route(const KeySpan &ks, const RouteTable &t, uint64_t *cand, 
     per_cu = per_cu < 1 ? 1 : per_cu > 8 ? 8 : per_cu;  // 8 x 256 threads = 32 waves per CU
     if (const char *e = getenv("BLOOMHIP_ROUTE_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
     const unsigned grid = grid_for(nw, kRouteBlock / 64, (unsigned)(device_cu_count() * per_cu));
-#define ROUTE_LAUNCH(L, F) \
-    k_route<L, F><<<grid, kRouteBlock, F ? lds : 0, stream>>>(ks, t, cand, nw, first, page)
-    if (ks.layout == KEYS_PACKED) {
-        if (in_lds) ROUTE_LAUNCH(KEYS_PACKED, true); else ROUTE_LAUNCH(KEYS_PACKED, false);
-    } else {
-        if (in_lds) ROUTE_LAUNCH(KEYS_STRIDED, true); else ROUTE_LAUNCH(KEYS_STRIDED, false);
+#define ROUTE_LAUNCH(L, F, R) \
+    k_route<L, F, R><<<grid, kRouteBlock, F ? lds : 0, stream>>>(ks, t, cand, nw, first, page)
+#define ROUTE_NR(L, F)                                                          \
+    switch (t.nruns) {                                                          \
+        case 1: ROUTE_LAUNCH(L, F, 1); break;                                   \
+        case 2: ROUTE_LAUNCH(L, F, 2); break;                                   \
+        case 3: ROUTE_LAUNCH(L, F, 3); break;                                   \
+        case 4: ROUTE_LAUNCH(L, F, 4); break;                                   \
+        case 5: ROUTE_LAUNCH(L, F, 5); break;                                   \
+        case 6: ROUTE_LAUNCH(L, F, 6); break;                                   \
+        case 7: ROUTE_LAUNCH(L, F, 7); break;                                   \
+        case 8: ROUTE_LAUNCH(L, F, 8); break;                                   \
+        default: ROUTE_LAUNCH(L, F, 0); break;                                  \
     }
+    if (ks.layout == KEYS_PACKED) {
+        if (in_lds) ROUTE_NR(KEYS_PACKED, true) else ROUTE_LAUNCH(KEYS_PACKED, false, 0);
+    } else {
+        if (in_lds) ROUTE_NR(KEYS_STRIDED, true) else ROUTE_LAUNCH(KEYS_STRIDED, false, 0);
+    }
+#undef ROUTE_NR
 #undef ROUTE_LAUNCH
     return hipGetLastError();
 }

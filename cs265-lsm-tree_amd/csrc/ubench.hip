@@ -252,7 +252,7 @@ bool ub_stack_plan(int nf, const uint64_t *ms, uint64_t *mmax, PartitionWorkspac
         *mmax = ms[j] > *mmax ? ms[j] : *mmax;
         g = g == 0 || ms[j] < g ? ms[j] : g;
     }
-    return plan_stack(*mmax, g, nf, device_cu_count(), ws);
+    return plan_stack(*mmax, g, g, nf, device_cu_count(), ws);
 }
 }  // namespace
 
@@ -283,7 +283,7 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
     st.nf = nf;
     for (int j = 0; j < nf; j++) {
         st.words[j] = reinterpret_cast<const uint32_t *>(words[j]);
-        st.nseg[j] = (uint32_t)(ms[j] / ws.seg_bits);
+        st.mwords[j] = (uint32_t)(ms[j] / 32);
         st.row[j] = j;
     }
     const ModParams mp = make_mod_params(mmax);
@@ -294,7 +294,7 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
     do {                                                                                           \
         (void)hipFuncSetAttribute(                                                                 \
             reinterpret_cast<const void *>(&k_part_apply<kApplyStack, G, A, B, kApplyDepth, TP>),  \
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kSegMaxBits / 8));                   \
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kStackMaxBits / 8));                 \
         k_part_apply<kApplyStack, G, A, B, kApplyDepth, TP><<<(unsigned)ws.nbins, B, lds, s>>>(    \
             ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, mmax, nullptr, 0,   \
             0, res, T);                                                                            \

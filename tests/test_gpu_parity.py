@@ -7,6 +7,10 @@ full-size configs compare with the SHA-256 fixtures the pinned oracle wrote
 negatives, idempotence, order independence, merge = union).
 """
 import hashlib
+import os
+import subprocess
+import sys
+import textwrap
 
 import numpy as np
 import pytest
@@ -326,6 +330,41 @@ def test_stacked_probe_with_cleared_and_empty_members(coracle):
     for j, (m, w) in enumerate(refs):
         assert (got[j] == coracle.test(w, m, probe)).all(), j
     assert not got[1].any() and not got[2].any()
+
+
+def test_stacked_probe_wraparound_windows():
+    """BLOOMHIP_STACK_WRAP=1 (read once per process, so a child process):
+    segments that do not divide the smaller members, each member staged from
+    (b*w) mod m_j with wraparound, in up to 160 KiB of LDS."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent(f"""
+        import sys
+        sys.path[:0] = [{os.path.join(root, 'cs265-lsm-tree_amd')!r}, {os.path.join(root, 'oracle')!r}]
+        import numpy as np
+        import bloomhip as bh
+        from bloom_oracle import COracle
+        C = COracle()
+        rng = np.random.default_rng(9)
+        for ms in ([655_360 * 4**i for i in range(5)], [3 * 2**20, 2**20, 3 * 2**18, 2**18]):
+            fs, refs = [], []
+            for j, m in enumerate(ms):
+                keys = rng.integers(-2**31, 2**31, size=40_000, dtype=np.int64).astype(np.int32)
+                f = bh.BloomFilter(m)
+                f.set_probe_strategy(bh.PROBE_STACKED)
+                f.set_batch(keys)
+                fs.append(f)
+                refs.append((m, C.build(m, keys), keys))
+            probe = rng.integers(-2**31, 2**31, size=300_001, dtype=np.int64).astype(np.int32)
+            for j, (m, w, keys) in enumerate(refs):
+                probe[j * 1000:(j + 1) * 1000] = keys[:1000]
+            got = bh.test_batch(fs, probe)
+            for j, (m, w, keys) in enumerate(refs):
+                assert (got[j] == C.test(w, m, probe)).all(), (ms, j)
+        print("ok")
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
+                       env={**os.environ, "BLOOMHIP_STACK_WRAP": "1"})
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
 
 
 def test_stacked_probe_profile_slot():
