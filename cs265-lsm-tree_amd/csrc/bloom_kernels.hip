@@ -477,15 +477,23 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         // member j's bits (b*w + o) mod m_j for o < w: the w bits from
         // (b*w) mod m_j on, wrapping at m_j (w <= m_j; w and m_j are
         // multiples of 128 bits, so no 16-B vector straddles the wrap)
-        for (int j = 0; j < st.nf; j++) {
+        // Word-interleaved image: member j's word p at seg[p * nf + j], so an
+        // entry's nf words sit together and one address (+ immediate offsets)
+        // reaches all of them.
+        const int nf = st.nf;
+        for (int j = 0; j < nf; j++) {
             const uint32_t mw = st.mwords[j];
             const uint32_t start = (uint32_t)(((uint64_t)b * seg_words) % mw);
             const uint4 *src = reinterpret_cast<const uint4 *>(st.words[j]);
-            uint4 *dst = reinterpret_cast<uint4 *>(seg + (size_t)j * seg_words);
             for (int i = threadIdx.x; i < (int)seg_words / 4; i += BLOCK) {
                 uint32_t wi = start + 4u * (uint32_t)i;
                 if (wi >= mw) wi -= mw;
-                dst[i] = src[wi / 4];
+                const uint4 v = src[wi / 4];
+                uint32_t *dst = seg + (size_t)(4 * i) * nf + j;
+                dst[0] = v.x;
+                dst[nf] = v.y;
+                dst[2 * nf] = v.z;
+                dst[3 * nf] = v.w;
             }
         }
     } else if constexpr (MODE == kApplyProbe) {
@@ -547,23 +555,17 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             const uint32_t o[4] = {v.x - base, v.y - base, v.z - base, v.w - base};
             uint32_t bits = 0, mask = 0;
             if constexpr (MODE == kApplyStack) {
-                uint32_t oo[4], r[4] = {0u, 0u, 0u, 0u};
+                uint32_t r[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const uint32_t ok = o[k] < lim ? 1u : 0u;
                     mask |= ok << k;
-                    oo[k] = ok ? o[k] : 0u;
-                }
+                    const uint32_t oo = ok ? o[k] : 0u;
+                    const uint32_t *wp = seg + __umul24(oo >> 5, (uint32_t)st.nf);
+                    const uint32_t sh = oo & 31;
 #pragma unroll
-                for (int j = 0; j < kMaxStack; j++) {
-                    if (j < st.nf) {
-                        const uint32_t *img = seg + (size_t)j * seg_words;
-                        uint32_t w[4];
-#pragma unroll
-                        for (int k = 0; k < 4; k++) w[k] = img[oo[k] >> 5];
-#pragma unroll
-                        for (int k = 0; k < 4; k++) r[k] |= ((w[k] >> (oo[k] & 31)) & 1u) << j;
-                    }
+                    for (int j = 0; j < kMaxStack; j++)  // member j's word at immediate offset 4j
+                        if (j < st.nf) r[k] |= __builtin_amdgcn_ubfe(wp[j], sh, 1u) << j;
                 }
 #pragma unroll
                 for (int k = 0; k < 4; k++) bits |= (mask >> k & 1u) ? r[k] << (8 * k) : 0u;
