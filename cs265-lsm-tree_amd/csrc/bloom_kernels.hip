@@ -445,8 +445,8 @@ inline int apply_lanes_per_tile(size_t nbins, size_t tile_pos = kPartTilePos) {
 // while the current one is applied, and the rare tile whose run outlasts the
 // first step is finished by a wave-uniform loop.
 // ABLATE (timing builds only): 1 = skip the LDS ORs (build), 2 = skip the
-// result stores (probe), 3 = non-temporal position loads.  The product
-// launches 0.
+// result stores (probe), 3 = non-temporal position loads, 4 = stage the LDS
+// image and stop.  The product launches 0.
 constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2;
 
 template <int MODE, int G, int ABLATE = 0, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth,
@@ -504,6 +504,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             reinterpret_cast<uint4 *>(seg)[i] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
+    if constexpr (ABLATE == 4) return;  // timing builds: staging only
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;

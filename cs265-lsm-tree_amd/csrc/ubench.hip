@@ -299,6 +299,19 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
             ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, mmax, nullptr, 0,   \
             0, res, T);                                                                            \
     } while (0)
+#define UB_STACKD(G, D)                                                                            \
+    do {                                                                                           \
+        if (ws.tile_keys == 2 * kPartTileKeys) {                                                   \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(                              \
+                &k_part_apply<kApplyStack, G, 0, kApplyBlock, D, 2 * kPartTilePos>),               \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kStackMaxBits / 8));             \
+            k_part_apply<kApplyStack, G, 0, kApplyBlock, D, 2 * kPartTilePos>                      \
+                <<<(unsigned)ws.nbins, kApplyBlock, lds, s>>>(ws.pos, ws.run_starts,               \
+                (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, mmax, nullptr, 0, 0, res, st);         \
+        } else {                                                                                   \
+            return -22;                                                                            \
+        }                                                                                          \
+    } while (0)
 #define UB_STACKB(G, A, T, B)                                                                      \
     do {                                                                                           \
         if (ws.tile_keys == 2 * kPartTileKeys) UB_STACKT(G, A, T, B, 2 * kPartTilePos);            \
@@ -329,6 +342,12 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
         case 10:
             if (G == 4) UB_STACKB(4, 2, st, 512); else if (G == 8) UB_STACKB(8, 2, st, 512); else return -22;
             break;
+        case 11:  // image staging only
+            if (G == 8) UB_STACK(8, 4, st); else return -22;
+            break;
+        case 201: UB_STACKD(8, 1); break;
+        case 203: UB_STACKD(8, 3); break;
+        case 204: UB_STACKD(8, 4); break;
         case 102: UB_STACK(2, 0, st); break;
         case 104: UB_STACK(4, 0, st); break;
         case 108: UB_STACK(8, 0, st); break;
@@ -338,5 +357,6 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
 #undef UB_STACK
 #undef UB_STACKB
 #undef UB_STACKT
+#undef UB_STACKD
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

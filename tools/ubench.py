@@ -196,7 +196,9 @@ def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
              3: "pass 2, no result stores", 4: "pass 2, member 0 image only", 5: "combine",
              6: "pass 2, non-temporal position loads",
              102: "pass 2 G=2", 104: "pass 2 G=4", 108: "pass 2 G=8", 116: "pass 2 G=16",
-             8: "pass 2, 512-thread blocks", 10: "pass 2, 512-thread blocks, no result stores"}
+             8: "pass 2, 512-thread blocks", 10: "pass 2, 512-thread blocks, no result stores",
+             11: "pass 2, image staging only", 201: "pass 2 G=8 depth 1",
+             203: "pass 2 G=8 depth 3", 204: "pass 2 G=8 depth 4"}
     for v in names:
         if run(v) != 0:
             continue
