@@ -815,11 +815,42 @@ __global__ void __launch_bounds__(kMetaBlock) k_run_meta(KeySpan ks, int32_t *__
     int32_t *fences = meta + 1;
     __shared__ int32_t s_max[kMetaBlock / 64];
     int32_t mx = INT32_MIN;
-    for (size_t i = (size_t)blockIdx.x * kMetaBlock + threadIdx.x; i < ks.n;
-         i += (size_t)gridDim.x * kMetaBlock) {
-        int32_t k;
-        if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
-        else k = load_key(ks, i);
+    // Packed keys and entry_t runs: 4 consecutive keys per lane per step (one
+    // 16-B load, or four 8-B entry loads), two steps in flight; a fence is
+    // always the first key of a step (kFenceStride % 4 == 0).
+    constexpr bool VEC = LAYOUT == KEYS_PACKED || LAYOUT == KEYS_ENTRY;
+    const size_t nthreads = (size_t)gridDim.x * kMetaBlock;
+    const size_t tid = (size_t)blockIdx.x * kMetaBlock + threadIdx.x;
+    size_t done = 0;
+    if constexpr (VEC) {
+        static_assert(kFenceStride % 4 == 0, "fences at step starts");
+        const size_t nq = ks.n / 4;
+        const bool a16 = (reinterpret_cast<uintptr_t>(ks.base) & 15) == 0;
+        auto quad = [&](size_t q) -> int4 {
+            if constexpr (LAYOUT == KEYS_PACKED) return reinterpret_cast<const int4 *>(ks.base)[q];
+            if (a16) {  // two entries per 16-B load
+                const int4 *e = reinterpret_cast<const int4 *>(ks.base) + 2 * q;
+                const int4 u = e[0], w = e[1];
+                return make_int4(u.x, u.z, w.x, w.z);
+            }
+            const int2 *e = reinterpret_cast<const int2 *>(ks.base) + 4 * q;
+            return make_int4(e[0].x, e[1].x, e[2].x, e[3].x);
+        };
+        auto take = [&](size_t q, const int4 &v) {
+            if ((4 * q) % kFenceStride == 0) fences[4 * q / kFenceStride] = v.x;
+            mx = max(mx, max(max(v.x, v.y), max(v.z, v.w)));
+        };
+        size_t q = tid;
+        for (; q + nthreads < nq; q += 2 * nthreads) {
+            const int4 a = quad(q), c = quad(q + nthreads);
+            take(q, a);
+            take(q + nthreads, c);
+        }
+        if (q < nq) take(q, quad(q));
+        done = nq * 4;
+    }
+    for (size_t i = done + tid; i < ks.n; i += nthreads) {
+        const int32_t k = load_key(ks, i);
         if (i % kFenceStride == 0) fences[i / kFenceStride] = k;
         mx = max(mx, k);
     }
@@ -1357,9 +1388,11 @@ hipError_t launch_run_meta(const KeySpan &ks, int32_t *meta, hipStream_t stream)
     hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(meta), (int)INT32_MIN, 1,
                                      stream);
     if (e != hipSuccess || ks.n == 0) return e;
-    const unsigned grid = grid_for(ks.n, kMetaBlock * 8, 1024);
+    const unsigned grid = grid_for(ks.n, kMetaBlock * 32, 2048);
     if (ks.layout == KEYS_PACKED)
         k_run_meta<KEYS_PACKED><<<grid, kMetaBlock, 0, stream>>>(ks, meta);
+    else if (ks.layout == KEYS_ENTRY)
+        k_run_meta<KEYS_ENTRY><<<grid, kMetaBlock, 0, stream>>>(ks, meta);
     else
         k_run_meta<KEYS_STRIDED><<<grid, kMetaBlock, 0, stream>>>(ks, meta);
     return hipGetLastError();

@@ -48,6 +48,10 @@ __device__ __forceinline__ uint64_t merge_path(GetA a_key, uint64_t na, GetB b_k
     return lo;
 }
 
+// One thread per tile boundary, a binary merge-path search.  (A 64-ary
+// search by one wave per boundary, 4 rounds instead of 23 dependent loads,
+// was slower at C3's fan-in: 31 vs 22 us, since its 128 scattered loads per
+// round miss where the serial searches' first levels share cached lines.)
 __global__ void k_merge_split(const Entry *__restrict__ a, uint64_t na,
                               const Entry *__restrict__ b, uint64_t nb, uint64_t ntiles,
                               uint64_t *__restrict__ split) {
@@ -92,16 +96,33 @@ __global__ void __launch_bounds__(kMergeBlock) k_merge_tile(const Entry *__restr
 }
 
 // Keep entry i when it is the first (newest) of its key, and not a dropped
-// tombstone.
-__device__ __forceinline__ bool keep(const Entry *e, uint64_t i, int drop_tombstones) {
-    const Entry x = e[i];
-    if (i > 0 && e[i - 1].key == x.key) return false;
-    return !(drop_tombstones && x.val == kTombstone);
-}
-
+// tombstone.  A dedup tile is kCompactRounds rounds of kCompactBlock lanes x 2
+// entries: lane l of round r owns entries 2l, 2l + 1 of the round's 512, read
+// as one 16-B vector (coalesced), plus the key before them.
 constexpr int kCompactBlock = 256;
-constexpr int kCompactIpt = 8;
-constexpr int kCompactTile = kCompactBlock * kCompactIpt;
+constexpr int kCompactRounds = 8;
+constexpr int kCompactTile = kCompactBlock * 2 * kCompactRounds;  // 4096 entries
+
+struct Pair {
+    Entry e0, e1;
+    uint32_t k0, k1;  // keep flags
+};
+
+__device__ __forceinline__ Pair load_pair(const Entry *__restrict__ e, uint64_t n, uint64_t i,
+                                          int drop) {
+    Pair p{};
+    if (i + 1 < n) {
+        const int4 v = *reinterpret_cast<const int4 *>(e + i);  // i even: 16-B aligned
+        p.e0 = Entry{v.x, v.y};
+        p.e1 = Entry{v.z, v.w};
+    } else if (i < n) {
+        p.e0 = e[i];
+    }
+    const int32_t prev = i > 0 && i < n ? e[i - 1].key : 0;
+    p.k0 = i < n && (i == 0 || prev != p.e0.key) && !(drop && p.e0.val == kTombstone);
+    p.k1 = i + 1 < n && p.e1.key != p.e0.key && !(drop && p.e1.val == kTombstone);
+    return p;
+}
 
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *s_w,
                                                          uint32_t *total) {
@@ -128,10 +149,14 @@ __global__ void __launch_bounds__(kCompactBlock) k_compact_count(const Entry *__
                                                                  uint64_t n, int drop,
                                                                  uint32_t *__restrict__ counts) {
     __shared__ uint32_t s_w[kCompactBlock / 64];
-    const uint64_t base = (uint64_t)blockIdx.x * kCompactTile + (uint64_t)threadIdx.x * kCompactIpt;
+    const uint64_t base = (uint64_t)blockIdx.x * kCompactTile + 2 * (uint64_t)threadIdx.x;
+    Pair p[kCompactRounds];
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; r++)  // every load issued before any is used
+        p[r] = load_pair(e, n, base + (uint64_t)r * 2 * kCompactBlock, drop);
     uint32_t c = 0;
-    for (int k = 0; k < kCompactIpt; k++)
-        if (base + k < n && keep(e, base + k, drop)) c++;
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; r++) c += p[r].k0 + p[r].k1;
     uint32_t total;
     (void)block_exclusive_scan(c, s_w, &total);
     if (threadIdx.x == 0) counts[blockIdx.x] = total;
@@ -158,20 +183,27 @@ __global__ void __launch_bounds__(1024) k_scan_counts(uint32_t *__restrict__ cou
     if (threadIdx.x == 0) counts[nblocks] = (uint32_t)s_carry;
 }
 
+// Kept entries leave in input order: per round, an exclusive scan of the
+// lanes' kept counts places them, so a wave's stores cover one contiguous
+// range of the output.
 __global__ void __launch_bounds__(kCompactBlock) k_compact_write(
     const Entry *__restrict__ e, uint64_t n, int drop, const uint32_t *__restrict__ offsets,
     Entry *__restrict__ out) {
     __shared__ uint32_t s_w[kCompactBlock / 64];
-    const uint64_t base = (uint64_t)blockIdx.x * kCompactTile + (uint64_t)threadIdx.x * kCompactIpt;
-    bool kf[kCompactIpt];
-    uint32_t c = 0;
-    for (int k = 0; k < kCompactIpt; k++) {
-        kf[k] = base + k < n && keep(e, base + k, drop);
-        c += kf[k];
+    const uint64_t base = (uint64_t)blockIdx.x * kCompactTile + 2 * (uint64_t)threadIdx.x;
+    Pair p[kCompactRounds];
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; r++)
+        p[r] = load_pair(e, n, base + (uint64_t)r * 2 * kCompactBlock, drop);
+    uint64_t run = offsets[blockIdx.x];
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; r++) {
+        uint32_t total;
+        const uint64_t pos = run + block_exclusive_scan(p[r].k0 + p[r].k1, s_w, &total);
+        if (p[r].k0) out[pos] = p[r].e0;
+        if (p[r].k1) out[pos + p[r].k0] = p[r].e1;
+        run += total;
     }
-    uint32_t pos = offsets[blockIdx.x] + block_exclusive_scan(c, s_w, nullptr);
-    for (int k = 0; k < kCompactIpt; k++)
-        if (kf[k]) out[pos++] = e[base + k];
 }
 
 }  // namespace
