@@ -28,8 +28,10 @@ def per_kernel(d):
             continue
         if base == "k_part_apply" and not name.startswith("k_part_apply<0"):  # probe modes
             continue
-        if base == "k_part_bin" and ", true," in name.split(">")[0].split("<", 1)[1][:20]:
-            continue  # SLOTS (probe) variant
+        if base == "k_part_bin":
+            targs = [a.strip() for a in name.split("<", 1)[1].split(">")[0].split(",")]
+            if len(targs) > 2 and targs[2] == "true":
+                continue  # SLOTS (probe) variant: k_part_bin<LAYOUT, ABLATE, SLOTS, COLS, TB>
         if base not in best or int(grid) > best[base][0]:
             best[base] = (int(grid), name, ctrs)
     return best
