@@ -28,8 +28,14 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// Key i of a span.  The layout is a template argument wherever the kernel
+// has one, so entry_t runs (stride 8) address as base + 8i instead of a
+// runtime 64-bit stride multiply.
+template <int LAYOUT = KEYS_STRIDED>
 __device__ __forceinline__ int32_t load_key(const KeySpan &ks, size_t i) {
-    return *reinterpret_cast<const int32_t *>(ks.base + i * ks.stride);
+    if constexpr (LAYOUT == KEYS_PACKED) return reinterpret_cast<const int32_t *>(ks.base)[i];
+    else if constexpr (LAYOUT == KEYS_ENTRY) return reinterpret_cast<const int2 *>(ks.base)[i].x;
+    else return *reinterpret_cast<const int32_t *>(ks.base + i * ks.stride);
 }
 
 __device__ __forceinline__ uint32_t pos32(uint64_t raw, const ModParams &mp) {
@@ -72,8 +78,8 @@ __global__ void __launch_bounds__(kBlock) k_build_atomic(KeySpan ks, ModParams m
             const int4 b = reinterpret_cast<const int4 *>(ks.base)[2 * q + 1];
             k0 = a.x; k1 = a.z; k2 = b.x; k3 = b.z;
         } else {
-            k0 = load_key(ks, 4 * q); k1 = load_key(ks, 4 * q + 1);
-            k2 = load_key(ks, 4 * q + 2); k3 = load_key(ks, 4 * q + 3);
+            k0 = load_key<LAYOUT>(ks, 4 * q); k1 = load_key<LAYOUT>(ks, 4 * q + 1);
+            k2 = load_key<LAYOUT>(ks, 4 * q + 2); k3 = load_key<LAYOUT>(ks, 4 * q + 3);
         }
         set3_global(words, k0, mp);
         set3_global(words, k1, mp);
@@ -82,7 +88,7 @@ __global__ void __launch_bounds__(kBlock) k_build_atomic(KeySpan ks, ModParams m
     }
     // tail (< 4 keys)
     const size_t t = nquads * 4 + tid;
-    if (t < ks.n) set3_global(words, load_key(ks, t), mp);
+    if (t < ks.n) set3_global(words, load_key<LAYOUT>(ks, t), mp);
 }
 
 // ---------------------------------------------------------------------------
@@ -101,7 +107,7 @@ __global__ void __launch_bounds__(kBlock) k_build_lds(KeySpan ks, ModParams mp,
     for (size_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
         int32_t k;
         if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
-        else k = load_key(ks, i);
+        else k = load_key<LAYOUT>(ks, i);
         const uint32_t p1 = pos32(raw_hash1(k), mp);
         const uint32_t p2 = pos32(raw_hash2(k), mp);
         const uint32_t p3 = pos32(raw_hash3(k), mp);
@@ -154,7 +160,7 @@ __device__ __forceinline__ void load_tile_keys(const KeySpan &ks, size_t tile, i
         const size_t i = tile0 + (size_t)j * TB + tid;
         if (i < ks.n) {
             if constexpr (LAYOUT == KEYS_PACKED) k[j] = reinterpret_cast<const int32_t *>(ks.base)[i];
-            else k[j] = load_key(ks, i);
+            else k[j] = load_key<LAYOUT>(ks, i);
         } else {
             k[j] = 0;
         }
@@ -670,7 +676,7 @@ __global__ void __launch_bounds__(kBlock) k_probe(KeySpan ks, ProbeTable t,
         int32_t k = 0;
         if (valid) {
             if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
-            else k = load_key(ks, i);
+            else k = load_key<LAYOUT>(ks, i);
         }
         const uint64_t h[3] = {raw_hash1(k), raw_hash2(k), raw_hash3(k)};
         for (int g = 0; g < t.nf; g += kProbeGroup) {
@@ -732,7 +738,7 @@ __global__ void __launch_bounds__(kProbeLdsBlock) k_probe_lds(KeySpan ks, const 
         int32_t k = 0;
         if (valid) {
             if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
-            else k = load_key(ks, i);
+            else k = load_key<LAYOUT>(ks, i);
         }
         const uint32_t p1 = mod_fast(raw_hash1(k), mp);
         const uint32_t p2 = mod_fast(raw_hash2(k), mp);
@@ -780,7 +786,8 @@ __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nf = rows.nf;
-    const int my_row = lane < nf ? rows.row[lane] : 0;
+    // lane f < nf stores member f's words: its row, this tile's first word
+    uint64_t *dst = out + (size_t)(lane < nf ? rows.row[lane] : 0) * nw + tile0 / 64 + wave;
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         const int key = j * kCombineBlock + (int)threadIdx.x;
@@ -791,7 +798,7 @@ __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
             const uint64_t ballot = __ballot((hit >> f) & 1u);
             if (lane == f) mine = ballot;
         }
-        if (lane < nf && base < tile_keys) out[(size_t)my_row * nw + (tile0 + base) / 64] = mine;
+        if (lane < nf && base < tile_keys) dst[j * (kCombineBlock / 64)] = mine;
     }
 }
 
@@ -850,7 +857,7 @@ __global__ void __launch_bounds__(kMetaBlock) k_run_meta(KeySpan ks, int32_t *__
         done = nq * 4;
     }
     for (size_t i = done + tid; i < ks.n; i += nthreads) {
-        const int32_t k = load_key(ks, i);
+        const int32_t k = load_key<LAYOUT>(ks, i);
         if (i % kFenceStride == 0) fences[i / kFenceStride] = k;
         mx = max(mx, k);
     }
@@ -939,7 +946,7 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
     auto load_key_at = [&](size_t ww) -> int32_t {
         const size_t i = min(min(ww, nw - 1) * 64 + lane, ks.n - 1);  // ks.n >= 1 here
         if constexpr (LAYOUT == KEYS_PACKED) return reinterpret_cast<const int32_t *>(ks.base)[i];
-        else return load_key(ks, i);
+        else return load_key<LAYOUT>(ks, i);
     };
     auto load_cand_at = [&](size_t ww) -> uint64_t {
         return cand[(size_t)min(lane, nruns - 1) * nw + min(ww, nw - 1)];
