@@ -594,9 +594,21 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             } else if (mask == 0xFu) {
                 *reinterpret_cast<uint32_t *>(p) = bits;
             } else if (mask != 0) {
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    if (mask & (1u << k)) p[k] = (uint8_t)(bits >> (8 * k));
+                // a run edge: each aligned half that is wholly this segment's
+                // goes out as one 2-byte store, the rest byte by byte
+                // (p is 4-byte aligned: e is a multiple of 4)
+                if ((mask & 3u) == 3u) {
+                    *reinterpret_cast<uint16_t *>(p) = (uint16_t)bits;
+                } else {
+                    if (mask & 1u) p[0] = (uint8_t)bits;
+                    if (mask & 2u) p[1] = (uint8_t)(bits >> 8);
+                }
+                if ((mask & 12u) == 12u) {
+                    *reinterpret_cast<uint16_t *>(p + 2) = (uint16_t)(bits >> 16);
+                } else {
+                    if (mask & 4u) p[2] = (uint8_t)(bits >> 16);
+                    if (mask & 8u) p[3] = (uint8_t)(bits >> 24);
+                }
             }
         } else {
             apply1(v.x, t, e);

@@ -103,6 +103,38 @@ def test_route_matches_oracle(coracle, probe):
     assert (first >= 0).sum() > 0 and (page[first >= 0] >= 0).all()
 
 
+def test_route_skewed_and_duplicate_fences(coracle):
+    """Runs whose keys are far from uniform (a dense cluster plus a sparse
+    tail), so the interpolation guess of k_route's page search misses and the
+    full binary search runs; runs with long stretches of equal keys (equal
+    fences: upper_bound must pass them all); GETs at, just below and just
+    above every fence."""
+    rng = np.random.default_rng(21)
+    dense = rng.integers(0, 200_000, size=270_000, dtype=np.int64)
+    tail = rng.integers(-2**31, 2**31, size=30_000, dtype=np.int64)
+    skewed = np.sort(np.concatenate([dense, tail])).astype(np.int32)
+    dup = np.sort(np.repeat(rng.integers(-2**31, 2**31, size=40, dtype=np.int64), 5000)).astype(np.int32)
+    small = np.sort(rng.integers(-1000, 1000, size=9000, dtype=np.int64)).astype(np.int32)
+    runs, refs = [], []
+    for keys in (small, skewed, dup):
+        m = bh.m_bits(keys.size, 10.0)
+        f = bh.BloomFilter(m)
+        f.set_batch_run(keys)
+        runs.append(f)
+        refs.append((keys, m))
+    fences = np.concatenate([k[::4096] for k, _ in refs]).astype(np.int64)
+    edge = np.concatenate([fences - 1, fences, fences + 1])
+    edge = np.clip(edge, -2**31, 2**31 - 1).astype(np.int32)
+    pool = np.concatenate([k for k, _ in refs])
+    gets = np.concatenate([edge, pool[rng.integers(0, pool.size, size=150_000)],
+                           rng.integers(-2**31, 2**31, size=50_000, dtype=np.int64).astype(np.int32)])
+    rng.shuffle(gets)
+    cand, first, page = bh.route_gets(runs, gets)
+    wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
+    assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
+    assert (page[first == 1] > 0).any()  # pages past the first in the skewed run
+
+
 def test_route_many_runs_and_missing_meta(coracle):
     """40 runs (probe launches chunked past 16 filters); one run has no
     metadata (never a candidate), one is empty."""
