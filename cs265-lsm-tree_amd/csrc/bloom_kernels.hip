@@ -1288,7 +1288,12 @@ template <int MODE, int TP>
 hipError_t launch_apply_tp(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                            uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                            hipStream_t stream) {
-    switch (apply_lanes_per_tile(ws.nbins, TP)) {
+    // BLOOMHIP_APPLY_LANES forces G (tuning experiments)
+    static const int g_env = [] {
+        const char *e = getenv("BLOOMHIP_APPLY_LANES");
+        return e ? atoi(e) : 0;
+    }();
+    switch (g_env ? g_env : apply_lanes_per_tile(ws.nbins, TP)) {
         case 2: return launch_apply_g<MODE, 2, TP>(ws, m, words, nw32, merge, res, st, stream);
         case 4: return launch_apply_g<MODE, 4, TP>(ws, m, words, nw32, merge, res, st, stream);
         case 8: return launch_apply_g<MODE, 8, TP>(ws, m, words, nw32, merge, res, st, stream);
