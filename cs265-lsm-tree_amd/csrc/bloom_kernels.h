@@ -55,13 +55,13 @@ constexpr size_t kLdsBitmapBytes = 160 * 1024;
 // Partition build geometry.  Pass 1 counting-sorts positions by sub-segment
 // p >> sub_shift (nsub <= kPartMaxBins sub-segments of 2^sub_shift bits).
 // Pass 2 gives each workgroup g consecutive sub-segments = one segment of
-// S = g << sub_shift bits (S <= kSegMaxBits, so it fits one workgroup's LDS);
+// S = g << sub_shift bits (S <= 160 KiB, so it fits one workgroup's LDS);
 // their runs are adjacent in every sorted tile, so a workgroup still reads one
 // contiguous run per tile.  plan_segments picks (sub_shift, g) so the number
 // of segments is a multiple of the CU count: every CU of pass 2 gets the same
 // share.
-constexpr uint32_t kSegMaxBits = 144u * 1024u * 8u;  // 144 KiB of LDS
-// A stacked probe's pass 2 has no static LDS: its images may use all 160 KiB.
+constexpr uint32_t kSegMaxBits = 144u * 1024u * 8u;  // 144 KiB of LDS (stacked-probe planes)
+// Pass 2 has no static LDS: segment images may use all 160 KiB (plan_segments).
 constexpr uint32_t kStackMaxBits = 160u * 1024u * 8u;
 constexpr int kPartBlock = 512;
 constexpr int kPartKPT = 8;  // keys per thread in pass 1
@@ -111,14 +111,16 @@ struct PartitionWorkspace {
 };
 
 // Keys per pass-1 tile for a batch sorted into nbins segments: short runs
-// (> 1024 segments: under 12 entries per segment and 4096-key tile) make
-// pass 2 line-bound, so such batches sort 8192-key tiles (one 1024-thread
-// workgroup per CU) and get runs twice as long (tools/ubench.py part_c4).
-// BLOOMHIP_BIG_TILE_BINS overrides the 1024 threshold (tuning experiments).
+// make pass 2 line-bound, so batches with more than 256 segments (under 48
+// entries per segment of a 4096-key tile) sort 8192-key tiles (one
+// 1024-thread workgroup per CU) and get runs twice as long: C3, C4 and C5
+// (C5: pass 2 0.302 -> 0.263 ms with 512 segments), while C2's 256 segments
+// keep 4096-key tiles (8192 cost C2 125 -> 112 Gkeys/s).
+// BLOOMHIP_BIG_TILE_BINS overrides the threshold (tuning experiments).
 inline uint32_t choose_tile_keys(size_t nbins) {
     static const size_t threshold = [] {
         const char *e = getenv("BLOOMHIP_BIG_TILE_BINS");
-        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)512;
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)256;
     }();
     return nbins > threshold ? 2 * (uint32_t)kPartTileKeys : (uint32_t)kPartTileKeys;
 }

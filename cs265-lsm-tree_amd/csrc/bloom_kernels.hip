@@ -1136,7 +1136,15 @@ int device_cu_count() {
 bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
     if (m == 0 || m > 0xFFFFFFFFull || ncu <= 0) return false;
     // Pass-2 segments: a multiple W of the CU count, each fitting in LDS.
-    const uint64_t per_round = (uint64_t)ncu * kSegMaxBits;
+    // Segment images up to all 160 KiB of a CU's LDS (pass 2 has no static
+    // LDS): C5 gets 512 segments instead of 768, runs 1.5x longer, pass 2
+    // 0.302 -> 0.263 ms.  BLOOMHIP_SEG_MAX_KIB (16..160) overrides (tuning).
+    static const uint64_t seg_max = [] {
+        const char *e = getenv("BLOOMHIP_SEG_MAX_KIB");
+        const uint64_t k = e ? strtoull(e, nullptr, 10) : 0;
+        return (k >= 16 && k <= 160) ? k * 1024 * 8 : (uint64_t)kStackMaxBits;
+    }();
+    const uint64_t per_round = (uint64_t)ncu * seg_max;
     const uint64_t W = ((m + per_round - 1) / per_round) * (uint64_t)ncu;
     // Sub-segments: the smallest power of two 2^s with at most kPartMaxBins
     // of them, then g = ceil(nsub / W) per segment, while g << s fits LDS.
@@ -1144,11 +1152,11 @@ bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
     while ((((m - 1) >> s) + 1) > kPartMaxBins) s++;
     uint64_t nsub = ((m - 1) >> s) + 1;
     uint64_t g = (nsub + W - 1) / W;
-    while (g > 1 && (g << s) > kSegMaxBits) g--;
-    if ((g << s) > kSegMaxBits) return false;
+    while (g > 1 && (g << s) > seg_max) g--;
+    if ((g << s) > seg_max) return false;
     // 128-B aligned segments for the 16-B segment stores.
     while (((g << s) % 1024) != 0) g++;
-    if ((g << s) > kSegMaxBits) return false;
+    if ((g << s) > seg_max) return false;
     ws->sub_shift = s;
     ws->group = (uint32_t)g;
     ws->nsub = (uint32_t)nsub;
@@ -1272,12 +1280,12 @@ hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *wo
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(
                                       &k_part_apply<MODE, G, 0, kApplyBlock, kApplyDepth, TP>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)((MODE == kApplyStack ? kStackMaxBits : kSegMaxBits) / 8));
+                                  (int)(kStackMaxBits / 8));
         return true;
     }();
     (void)attr_set;
     const size_t lds = (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
-    if (lds > (MODE == kApplyStack ? kStackMaxBits : kSegMaxBits) / 8) return hipErrorInvalidValue;
+    if (lds > kStackMaxBits / 8) return hipErrorInvalidValue;
     k_part_apply<MODE, G, 0, kApplyBlock, kApplyDepth, TP><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
         res, st);
