@@ -241,6 +241,60 @@ def probe_c3_sharded(torch, bh, dist, rank, world, steps, warmup, coll_dev):
             "note": "filters replicated per GPU, GET keys sharded contiguously, no data collective"}
 
 
+def c5_eight_runs(torch, bh, dist, rank, world, steps, warmup, coll_dev):
+    """BASELINE configs[4] / SURVEY §8d C5: 8 independent runs r = 0..7 of
+    67,108,864 keys (seed 13141 + r, 10 bits/key), run r built on rank
+    r % N, one after another on its GPU; no collective on the data path.
+    A step builds every run once; rate = 8 runs' keys / max over ranks of
+    the timed region, so N = 1, 2, 4, 8 time the same fixed job (strong
+    scaling of the fan-in).  Each run's bitmap is checked against its
+    pinned SHA-256 (tests/golden/pins.json)."""
+    from bloomhip import workloads as W
+    mine = [r for r in range(8) if r % world == rank]
+    built = []
+    for r in mine:
+        keys, m = W.c5_run(r)
+        dk = torch.from_numpy(keys).cuda()
+        del keys
+        f = bh.BloomFilter(m, device=torch.cuda.current_device())
+        built.append((r, dk, f))
+    s = torch.cuda.current_stream()
+
+    def step():
+        for _, dk, f in built:
+            f.clear(stream=s)
+            f.set_batch(dk, stream=s)
+    step()
+    torch.cuda.synchronize()
+    pins = None
+    pins_path = os.path.join(ROOT, "tests", "golden", "pins.json")
+    if os.path.exists(pins_path):
+        pins = json.load(open(pins_path))["oracle"]["c5"]
+    ok = all(pins is None or hashlib.sha256(f.words().tobytes()).hexdigest() == pins[r]["sha256"]
+             for r, _, f in built)
+    for _ in range(warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = (time.perf_counter() - t0) / steps
+    if dist:
+        from bloomhip import shard
+        el = shard.max_over_ranks(el, dist, device=coll_dev)
+        ok = shard.all_ranks_ok(ok, dist, device=coll_dev)
+    n_all = 8 * W.C5_N
+    return {"gkeys_s": round(n_all / el / 1e9, 3), "ms": round(el * 1e3, 4),
+            "runs_per_rank": len(mine), "keys_per_run": W.C5_N, "m_bits": built[0][2].m if built else None,
+            "verified_vs_oracle": bool(ok),
+            "note": "8 runs x 64M keys (configs[4]); run r on rank r % N; rate = all 8 runs / max-rank time"}
+
+
 def compact_fanin(torch, bh, reps):
     """§8f row 3: a fan-in-4 compaction (4 runs x 4M entries, newest first)
     merged on the device and fused with the new run's filter + fence build
@@ -299,6 +353,7 @@ def main():
     ap.add_argument("--strategy", default="auto", choices=["auto", "atomic", "lds", "partition"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip probe/e2e legs")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 eight-run leg")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -397,6 +452,12 @@ def main():
 
     extras = {}
     cpu = None
+    if not args.no_extras and not args.no_c5:
+        if rank == 0:
+            log("C5 eight runs ...")
+        extras["c5_eight_runs"] = c5_eight_runs(torch, bh, dist, rank, world,
+                                                max(3, args.steps // 20), 1, coll_dev)
+        torch.cuda.empty_cache()
     if world > 1 and not args.no_extras:
         if rank == 0:
             log("sharded probe C3 ...")
