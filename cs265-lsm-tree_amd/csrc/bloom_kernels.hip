@@ -196,7 +196,8 @@ __device__ __forceinline__ size_t part_tile(size_t k, size_t ntiles) {
 // COLS = true: straight into the segment-major table runs[b * ntiles + tile];
 // COLS = false: into the tile-major runs[tile * (nbins + 1) + b], for
 // k_runs_transpose (large tables: see there).
-template <int LAYOUT, int ABLATE = 0, bool SLOTS = false, bool COLS = true, int TB = kPartBlock>
+template <int LAYOUT, int ABLATE = 0, bool SLOTS = false, bool COLS = true, int TB = kPartBlock,
+          int STAGGER = 0>
 __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
                                                          uint32_t *__restrict__ pos_out,
                                                          uint32_t *__restrict__ runs,
@@ -355,6 +356,10 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
     // Full tiles in the loop; the short last tile (index ntiles - 1, always
     // in a block's final round) after it, so the loop sees only FULL.
     const size_t nfull = ks.n / kTileKeys;
+    if constexpr (STAGGER > 0) {  // timing builds (tools/ubench): delay the second half of the grid
+        if (blockIdx.x >= gridDim.x / 2)
+            for (int i = 0; i < STAGGER; i++) __builtin_amdgcn_s_sleep(127);
+    }
     size_t tile = part_tile(0, ntiles);
     if (tile < ntiles) load_tile_keys<LAYOUT, TB>(ks, tile, tid, kcur);
     size_t round = 0;

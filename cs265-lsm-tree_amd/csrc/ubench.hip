@@ -183,6 +183,12 @@ extern "C" int ubench_part_bin(int ablate, const void *keys, size_t n, uint64_t 
         case 7:  // pass 1 (columns) with one workgroup per CU, leaving LDS for a concurrent pass 2
             k_part_bin<KEYS_PACKED, 0, false, true><<<(unsigned)device_cu_count(), kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr);
             break;
+        // 8..10: the product's pass 1 with the second half of the grid
+        // started 1..3 x 8K cycles late (do the two workgroups of a CU run
+        // their VALU and LDS phases in step?)
+        case 8: k_part_bin<KEYS_PACKED, 0, false, true, kPartBlock, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 9: k_part_bin<KEYS_PACKED, 0, false, true, kPartBlock, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
+        case 10: k_part_bin<KEYS_PACKED, 0, false, true, kPartBlock, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
         default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -95,6 +95,41 @@ def part_ablation(n=16_777_216, bpe=10.0):
                               "us": round(a.elapsed_time(b) / 10 * 1e3, 2)}), flush=True)
 
 
+def part_stagger(n=16_777_216, bpe=10.0):
+    """Pass 1 (C2) as the product launches it (0), with one workgroup per CU
+    (7), and with the second half of the grid started late (8..10)."""
+    sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
+    import bloomhip as bh
+    keys = torch.from_numpy(bh.gen_puts(13141, n)).cuda()
+    m = bh.m_bits(n, bpe)
+    ntiles = (keys.numel() + 4095) // 4096
+    pos = torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda")
+    rs = torch.empty(ntiles * 4097 * 2, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    names = {0: "product", 7: "one workgroup per CU", 8: "stagger 8K cycles",
+             9: "stagger 16K cycles", 10: "stagger 24K cycles"}
+    ref = None
+    for ab in (0, 7, 8, 9, 10, 0):
+        for _ in range(3):
+            assert LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(),
+                                       rs.data_ptr(), s.cuda_stream) == 0
+        torch.cuda.synchronize()
+        same = None
+        if ab in (0, 8):
+            h = (pos.sum().item(), rs[:ntiles * 257].sum().item())
+            ref = h if ref is None else ref
+            same = h == ref
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(20):
+            LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(),
+                                rs.data_ptr(), s.cuda_stream)
+        b.record(s)
+        torch.cuda.synchronize()
+        print(json.dumps({"op": "k_part_bin", "variant": names[ab], "same_output": same,
+                          "us": round(a.elapsed_time(b) / 20 * 1e3, 2)}), flush=True)
+
+
 def overlap(n=16_777_216, bpe=10.0):
     """Does pass 1 of one half-batch overlap pass 2 of the other on two
     streams?  Times bin(A) apply(A) bin(B) apply(B) on one stream against
@@ -238,6 +273,8 @@ def main():
         return stack_ablation((0, 1, 2, 3))
     if len(sys.argv) > 1 and sys.argv[1] == "isa":
         return isa_rates()
+    if len(sys.argv) > 1 and sys.argv[1] == "stagger":
+        return part_stagger()
     if len(sys.argv) > 1 and sys.argv[1] == "part":
         return part_ablation()
     if len(sys.argv) > 1 and sys.argv[1] == "part_c5":
