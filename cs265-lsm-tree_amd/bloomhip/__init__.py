@@ -181,19 +181,67 @@ def host_positions(m: int, keys) -> np.ndarray:
     return out
 
 
+def _nbytes(buf) -> int:
+    return buf.nbytes if isinstance(buf, np.ndarray) else buf.numel() * buf.element_size()
+
+
+def _is_tensor(buf) -> bool:
+    # duck-typed so importing this module does not need torch
+    return hasattr(buf, "data_ptr") and hasattr(buf, "is_cuda")
+
+
 def _ptr_of(buf):
     """(address, on_device, keepalive) for a numpy array or a torch tensor."""
     if isinstance(buf, np.ndarray):
         if not buf.flags["C_CONTIGUOUS"]:
             buf = np.ascontiguousarray(buf)
         return buf.ctypes.data, 0, buf
-    # torch tensor (duck-typed so importing this module does not need torch)
-    if hasattr(buf, "data_ptr") and hasattr(buf, "is_cuda"):
+    if _is_tensor(buf):
         if not buf.is_contiguous():
             raise ValueError("tensor must be contiguous")
         return buf.data_ptr(), 1 if buf.is_cuda else 0, buf
     arr = np.ascontiguousarray(buf, dtype=np.int32)
     return arr.ctypes.data, 0, arr
+
+
+def _keys_ptr(keys, stride: int):
+    """_ptr_of for a key vector (KEY_t = int32, src/types.h:4).  The engine
+    reads int32 words at `stride` bytes; any other element type would be read
+    as the wrong keys, so: numpy integer arrays at stride 4 are converted to
+    int32 when every value fits, anything else that is not int32 is refused.
+    Strided views (e.g. entry_t runs at stride 8) must be int32 buffers."""
+    if isinstance(keys, np.ndarray):
+        if keys.dtype != np.int32:
+            if stride != 4 or keys.dtype.kind not in "iu":
+                raise ValueError(f"keys must be int32 (got {keys.dtype} at stride {stride})")
+            if keys.size and (keys.min() < -2**31 or keys.max() > 2**31 - 1):
+                raise ValueError("keys out of int32 range")
+            keys = keys.astype(np.int32)
+    elif _is_tensor(keys):
+        if str(keys.dtype) != "torch.int32":
+            raise ValueError(f"key tensor must be torch.int32 (got {keys.dtype})")
+    return _ptr_of(keys)
+
+
+def _key_count(keep, stride: int, n):
+    avail = _nbytes(keep)
+    if n is None:
+        return avail // stride
+    if n and (n - 1) * stride + 4 > avail:
+        raise ValueError(f"{n} keys at stride {stride} need more than the {avail} bytes given")
+    return n
+
+
+def _out_ptr(buf, need_bytes: int, itemsize: int, what: str):
+    """_ptr_of for an output buffer: element size and capacity checked."""
+    el = buf.itemsize if isinstance(buf, np.ndarray) else buf.element_size()
+    if el != itemsize:
+        raise ValueError(f"{what}: elements must be {itemsize} bytes (got {el})")
+    if _nbytes(buf) < need_bytes:
+        raise ValueError(f"{what}: {need_bytes} bytes needed, {_nbytes(buf)} given")
+    if isinstance(buf, np.ndarray) and not buf.flags["C_CONTIGUOUS"]:
+        raise ValueError(f"{what} must be contiguous")
+    return _ptr_of(buf)
 
 
 def _stream_ptr(stream):
@@ -285,20 +333,16 @@ class BloomFilter:
 
     # --- batches ----------------------------------------------------------
     def set_batch(self, keys, n: int | None = None, stride: int = 4, stream=None) -> None:
-        ptr, on_dev, keep = _ptr_of(keys)
-        if n is None:
-            nbytes = keep.nbytes if isinstance(keep, np.ndarray) else keep.numel() * keep.element_size()
-            n = nbytes // stride
+        ptr, on_dev, keep = _keys_ptr(keys, stride)
+        n = _key_count(keep, stride, n)
         _check(_lib().bloomhip_set_batch(self._h, ptr, n, stride, on_dev, _stream_ptr(stream)),
                "bloomhip_set_batch")
 
     def set_batch_run(self, keys, n: int | None = None, stride: int = 4, stream=None) -> None:
         """set() of a whole run written in this key order, plus its fence
         pointers and max key (Run::put, src/run.cpp:158-174)."""
-        ptr, on_dev, keep = _ptr_of(keys)
-        if n is None:
-            nbytes = keep.nbytes if isinstance(keep, np.ndarray) else keep.numel() * keep.element_size()
-            n = nbytes // stride
+        ptr, on_dev, keep = _keys_ptr(keys, stride)
+        n = _key_count(keep, stride, n)
         _check(_lib().bloomhip_set_batch_run(self._h, ptr, n, stride, on_dev,
                                              _stream_ptr(stream)), "bloomhip_set_batch_run")
 
@@ -382,15 +426,13 @@ def test_batch(filters: Sequence[BloomFilter], keys, n: int | None = None, strid
                out=None, stream=None):
     """is_set of every key against each filter.  Returns (or fills) a packed
     [nf, ceil(n/64)] uint64 array: bit i%64 of row j word i/64 = filters[j].is_set(key i)."""
-    ptr, on_dev, keep = _ptr_of(keys)
-    if n is None:
-        nbytes = keep.nbytes if isinstance(keep, np.ndarray) else keep.numel() * keep.element_size()
-        n = nbytes // stride
+    ptr, on_dev, keep = _keys_ptr(keys, stride)
+    n = _key_count(keep, stride, n)
     nf = len(filters)
     nw = (n + 63) // 64
     if out is None:
         out = np.zeros((nf, nw), dtype=np.uint64)
-    optr, out_dev, okeep = _ptr_of(out)
+    optr, out_dev, okeep = _out_ptr(out, nf * nw * 8, 8, "out")
     arr = (ctypes.c_void_p * nf)(*[f.handle.value for f in filters])
     _check(_lib().bloomhip_test_batch(arr, nf, ptr, n, stride, on_dev, optr, out_dev,
                                       _stream_ptr(stream)), "bloomhip_test_batch")
@@ -402,17 +444,17 @@ def route_gets(runs: Sequence[BloomFilter], keys, n: int | None = None, stride: 
     """Batched GET routing (bloomhip_route_gets): runs newest first.  Returns
     (cand [nruns, ceil(n/64)] uint64 packed, first int32[n], page int32[n]);
     pass device tensors for all three to keep the outputs on the device."""
-    ptr, on_dev, keep = _ptr_of(keys)
-    if n is None:
-        nbytes = keep.nbytes if isinstance(keep, np.ndarray) else keep.numel() * keep.element_size()
-        n = nbytes // stride
+    ptr, on_dev, keep = _keys_ptr(keys, stride)
+    n = _key_count(keep, stride, n)
     nr = len(runs)
     nw = (n + 63) // 64
     if cand is None and first is None and page is None:
         cand = np.zeros((nr, nw), dtype=np.uint64)
         first = np.empty(n, dtype=np.int32)
         page = np.empty(n, dtype=np.int32)
-    outs = [_ptr_of(x) if x is not None else (None, None, None) for x in (cand, first, page)]
+    need = ((nr * nw * 8, 8, "cand"), (n * 4, 4, "first"), (n * 4, 4, "page"))
+    outs = [_out_ptr(x, *nd) if x is not None else (None, None, None)
+            for x, nd in zip((cand, first, page), need)]
     devs = {o[1] for o in outs if o[0] is not None}
     if len(devs) > 1:
         raise ValueError("route_gets outputs must be all host or all device buffers")
@@ -431,17 +473,20 @@ def compact(runs, drop_tombstones: bool = False, filter: BloomFilter | None = No
     [n_out, 2] int32 array, or the first n_out rows of `out` when given);
     builds `filter` (and its run metadata) from the merged keys when given."""
     nr = len(runs)
+    for r in runs:  # entry_t {int32 key; int32 val;} (src/types.h:14-22)
+        dt = str(r.dtype)
+        if dt not in ("int32", "torch.int32") or len(r.shape) != 2 or r.shape[1] != 2:
+            raise ValueError(f"runs must be int32 [n, 2] entry_t arrays (got {dt} {tuple(r.shape)})")
     keeps = [_ptr_of(r) for r in runs]
     ons = {k[1] for k in keeps}
     if len(ons) > 1:
         raise ValueError("runs must be all host or all device buffers")
     on_dev = ons.pop() if ons else 0
-    sizes = [(k[2].nbytes if isinstance(k[2], np.ndarray) else k[2].numel() * k[2].element_size())
-             // 8 for k in keeps]
+    sizes = [_nbytes(k[2]) // 8 for k in keeps]
     total = sum(sizes)
     if out is None:
         out = np.empty((max(total, 1), 2), dtype=np.int32)
-    optr, out_dev, okeep = _ptr_of(out)
+    optr, out_dev, okeep = _out_ptr(out, total * 8, 4, "out")
     arr = (ctypes.c_void_p * max(nr, 1))(*[k[0] for k in keeps])
     ns = (ctypes.c_size_t * max(nr, 1))(*sizes)
     n_out = ctypes.c_size_t()

@@ -110,6 +110,10 @@ struct bloomhip_filter {
     uint32_t nfences = 0;
     void *d_route_stage = nullptr;  // first/page staging for host outputs
     size_t route_stage_bytes = 0;
+    // bloomhip_is_set's answer: a pinned host word mapped into the device
+    // (allocated on the first scalar call)
+    uint32_t *h_hit = nullptr;
+    uint32_t *d_hit = nullptr;
 
     bool prof = false;
     uint64_t prof_launches[BLOOMHIP_PROF_SLOTS] = {};
@@ -119,6 +123,27 @@ struct bloomhip_filter {
 };
 
 namespace {
+
+// Locks the distinct handles of a multi-filter call in one global order (by
+// address) and releases them in reverse, so concurrent calls over the same
+// filters in different orders ([a, b] and [b, a]) cannot deadlock.
+class HandleLocks {
+   public:
+    HandleLocks(const bloomhip_filter *const *fs, int n) {
+        for (int i = 0; i < n; i++) hs_.push_back(const_cast<bloomhip_filter *>(fs[i]));
+        std::sort(hs_.begin(), hs_.end(), std::less<bloomhip_filter *>());
+        hs_.erase(std::unique(hs_.begin(), hs_.end()), hs_.end());
+        for (bloomhip_filter *h : hs_) h->mu.lock();
+    }
+    ~HandleLocks() {
+        for (auto it = hs_.rbegin(); it != hs_.rend(); ++it) (*it)->mu.unlock();
+    }
+    HandleLocks(const HandleLocks &) = delete;
+    HandleLocks &operator=(const HandleLocks &) = delete;
+
+   private:
+    std::vector<bloomhip_filter *> hs_;
+};
 
 // NULL is HIP's default (null) stream, as everywhere in HIP: work given no
 // stream is ordered with the caller's other default-stream work (e.g. a torch
@@ -154,8 +179,11 @@ hipError_t grow_touched(void **ptr, size_t *have, size_t need, hipStream_t s) {
 // Scratch of the partition build / partitioned probe.  Shared by every handle
 // that runs on the same (device, stream): work on one stream is ordered, so
 // one set of buffers serves all of it, allocated (and first touched) once.
+// Lock order everywhere: filter handle(s) first, then the workspace.  The
+// workspace lock is recursive: a compaction holds it across the build of its
+// output run's filter, which takes it again (run_partition).
 struct Workspace {
-    std::mutex mu;  // held while work using the buffers is enqueued
+    std::recursive_mutex mu;  // held while work using the buffers is enqueued
     uint32_t *pos = nullptr;  // tile-sorted segment offsets
     size_t pos_bytes = 0;
     uint32_t *runs = nullptr;  // run starts: tile-major rows, then segment-major
@@ -354,7 +382,7 @@ int materialize_clear(bloomhip_filter *f, hipStream_t s) {
 
 int run_partition(bloomhip_filter *f, const KeySpan &ks, hipStream_t s) {
     Workspace *w = workspace_for(f->device, s);
-    std::lock_guard<std::mutex> lk(w->mu);
+    std::lock_guard<std::recursive_mutex> lk(w->mu);
     PartitionWorkspace ws{};
     int rc = partition_workspace(w, f->m, ks.n, s, &ws);
     if (rc) return rc;
@@ -457,6 +485,7 @@ int bloomhip_destroy(bloomhip_filter *f) {
     if (f->d_out_stage) (void)hipFree(f->d_out_stage);
     if (f->d_meta) (void)hipFree(f->d_meta);
     if (f->d_route_stage) (void)hipFree(f->d_route_stage);
+    if (f->h_hit) (void)hipHostFree(f->h_hit);
     (void)hipStreamDestroy(f->stream);
     delete f;
     return BLOOMHIP_OK;
@@ -577,13 +606,11 @@ int bloomhip_set_batch(bloomhip_filter *f, const void *keys, size_t n, size_t st
     return BLOOMHIP_OK;
 }
 
-int bloomhip_set_batch_run(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
-                           int keys_on_device, void *stream) {
-    g_last_error.clear();
-    if (!f) return BLOOMHIP_EINVAL;
-    DeviceGuard g(f->device);
-    std::lock_guard<std::mutex> lk(f->mu);
-    hipStream_t s = pick_stream(f, stream);
+namespace {
+
+// bloomhip_set_batch_run with f->mu held and f's device current.
+int set_batch_run_locked(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
+                         int keys_on_device, hipStream_t s) {
     KeySpan ks{};
     int rc = device_keys(f, keys, n, stride_bytes, keys_on_device, s, &ks);
     if (rc) return rc;
@@ -600,6 +627,17 @@ int bloomhip_set_batch_run(bloomhip_filter *f, const void *keys, size_t n, size_
     f->nfences = (uint32_t)nf;
     if (!keys_on_device) HIP_TRY(hipStreamSynchronize(s));
     return BLOOMHIP_OK;
+}
+
+}  // namespace
+
+int bloomhip_set_batch_run(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
+                           int keys_on_device, void *stream) {
+    g_last_error.clear();
+    if (!f) return BLOOMHIP_EINVAL;
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    return set_batch_run_locked(f, keys, n, stride_bytes, keys_on_device, pick_stream(f, stream));
 }
 
 int bloomhip_set_run_meta(bloomhip_filter *f, const int32_t *fences, size_t nfences,
@@ -710,7 +748,7 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
             st.row[k] = mem[k];
         }
         Workspace *w = workspace_for(f0->device, s);
-        std::lock_guard<std::mutex> wl(w->mu);
+        std::lock_guard<std::recursive_mutex> wl(w->mu);
         int rc = partition_buffers(w, n, s, &ws);
         if (rc) return rc;
         rc = probe_buffers(w, ws, s);
@@ -752,7 +790,7 @@ int probe_rows(bloomhip_filter *f0, const bloomhip_filter *const *filters, int n
             continue;
         }
         Workspace *w = workspace_for(f0->device, s);
-        std::lock_guard<std::mutex> wl(w->mu);
+        std::lock_guard<std::recursive_mutex> wl(w->mu);
         PartitionWorkspace ws{};
         rc = partition_workspace(w, filters[j]->m, n, s, &ws);
         if (rc) return rc;
@@ -784,18 +822,10 @@ int probe_rows(bloomhip_filter *f0, const bloomhip_filter *const *filters, int n
     return BLOOMHIP_OK;
 }
 
-// Deferred clears of every filter, issued on s (f0->mu held).
-int materialize_all(bloomhip_filter *f0, const bloomhip_filter *const *filters, int nf,
-                    hipStream_t s) {
+// Deferred clears of every filter, issued on s (every handle's lock held).
+int materialize_all(const bloomhip_filter *const *filters, int nf, hipStream_t s) {
     for (int j = 0; j < nf; j++) {
-        bloomhip_filter *fj = const_cast<bloomhip_filter *>(filters[j]);
-        int rc;
-        if (fj != f0) {
-            std::lock_guard<std::mutex> lj(fj->mu);
-            rc = materialize_clear(fj, s);
-        } else {
-            rc = materialize_clear(fj, s);
-        }
+        int rc = materialize_clear(const_cast<bloomhip_filter *>(filters[j]), s);
         if (rc) return rc;
     }
     return BLOOMHIP_OK;
@@ -813,12 +843,12 @@ int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const voi
     // Staging and profiling state live on the first handle.
     bloomhip_filter *f0 = const_cast<bloomhip_filter *>(filters[0]);
     DeviceGuard g(f0->device);
-    std::lock_guard<std::mutex> lk(f0->mu);
+    HandleLocks locks(filters, nf);
     hipStream_t s = pick_stream(f0, stream);
     KeySpan ks{};
     int rc = device_keys(f0, keys, n, stride_bytes, keys_on_device, s, &ks);
     if (rc) return rc;
-    rc = materialize_all(f0, filters, nf, s);
+    rc = materialize_all(filters, nf, s);
     if (rc) return rc;
     const size_t nw = (n + 63) / 64;
     const size_t out_bytes = (size_t)nf * nw * 8;
@@ -849,12 +879,12 @@ int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const voi
     if (n == 0) return BLOOMHIP_OK;
     bloomhip_filter *f0 = const_cast<bloomhip_filter *>(runs[0]);
     DeviceGuard g(f0->device);
-    std::lock_guard<std::mutex> lk(f0->mu);
+    HandleLocks locks(runs, nruns);
     hipStream_t s = pick_stream(f0, stream);
     KeySpan ks{};
     int rc = device_keys(f0, keys, n, stride_bytes, keys_on_device, s, &ks);
     if (rc) return rc;
-    rc = materialize_all(f0, runs, nruns, s);
+    rc = materialize_all(runs, nruns, s);
     if (rc) return rc;
     RouteTable t{};
     t.nruns = nruns;
@@ -862,12 +892,7 @@ int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const voi
     for (int j = 0; j < nruns; j++) {
         bloomhip_filter *fj = const_cast<bloomhip_filter *>(runs[j]);
         if (!fj->d_meta) {  // no metadata: never a candidate
-            if (fj != f0) {
-                std::lock_guard<std::mutex> lj(fj->mu);
-                rc = meta_reserve(fj, 0);
-            } else {
-                rc = meta_reserve(fj, 0);
-            }
+            rc = meta_reserve(fj, 0);
             if (rc) return rc;
             fj->nfences = 0;
         }
@@ -908,16 +933,39 @@ int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const voi
 
 int bloomhip_set(bloomhip_filter *f, int32_t key) {
     g_last_error.clear();
-    return bloomhip_set_batch(f, &key, 1, sizeof key, 0, nullptr);
+    if (!f) return BLOOMHIP_EINVAL;
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    hipStream_t s = nullptr;  // HIP's default stream, ordered with the caller's other work
+    int rc = materialize_clear(f, s);
+    if (rc) return rc;
+    hipError_t e = launch_set1(f->d_words, f->mp, key, s);
+    if (e != hipSuccess) return fail_hip(e, "k_set1 launch");
+    f->known_zero = false;
+    HIP_TRY(hipStreamSynchronize(s));
+    return BLOOMHIP_OK;
 }
 
-int bloomhip_is_set(const bloomhip_filter *f, int32_t key, int *hit_out) {
+int bloomhip_is_set(const bloomhip_filter *fc, int32_t key, int *hit_out) {
     g_last_error.clear();
-    if (!f || !hit_out) return BLOOMHIP_EINVAL;
-    uint64_t word = 0;
-    int rc = bloomhip_test_batch(&f, 1, &key, 1, sizeof key, 0, &word, 0, nullptr);
+    if (!fc || !hit_out) return BLOOMHIP_EINVAL;
+    bloomhip_filter *f = const_cast<bloomhip_filter *>(fc);
+    DeviceGuard g(f->device);
+    std::lock_guard<std::mutex> lk(f->mu);
+    if (!f->h_hit) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&f->h_hit), 64, hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&f->d_hit), f->h_hit, 0));
+    }
+    hipStream_t s = nullptr;
+    int rc = materialize_clear(f, s);
     if (rc) return rc;
-    *hit_out = (int)(word & 1u);
+    *reinterpret_cast<volatile uint32_t *>(f->h_hit) = 2u;  // overwritten by the kernel
+    hipError_t e = launch_is_set1(f->d_words, f->mp, key, f->d_hit, s);
+    if (e != hipSuccess) return fail_hip(e, "k_is_set1 launch");
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t v = *reinterpret_cast<volatile uint32_t *>(f->h_hit);
+    if (v > 1u) return fail_hip(hipErrorUnknown, "k_is_set1 result not visible");
+    *hit_out = (int)v;
     return BLOOMHIP_OK;
 }
 
@@ -1074,7 +1122,7 @@ int bloomhip_trim(void) {
     std::lock_guard<std::mutex> lk(g_ws_mu);
     for (auto &kv : g_ws) {
         Workspace *w = kv.second.get();
-        std::lock_guard<std::mutex> wl(w->mu);
+        std::lock_guard<std::recursive_mutex> wl(w->mu);
         DeviceGuard g(kv.first.first);
         (void)hipStreamSynchronize(kv.first.second);
         for (void *p : {(void *)w->pos, (void *)w->runs, (void *)w->res, (void *)w->slots,
@@ -1103,11 +1151,15 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
     if (device < 0 || device >= ndev) return BLOOMHIP_EINVAL;
     DeviceGuard g(device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const void *dout = nullptr;
     uint64_t kept = 0;
     {
+        // The merged run lives in the shared workspace (mbuf) until its filter
+        // is built and it is copied out, so the workspace stays locked until
+        // then (filter first, then workspace: the global lock order).
+        std::unique_lock<std::mutex> flk;
+        if (f) flk = std::unique_lock<std::mutex>(f->mu);
         Workspace *w = workspace_for(device, s);
-        std::lock_guard<std::mutex> wl(w->mu);
+        std::lock_guard<std::recursive_mutex> wl(w->mu);
         const size_t bytes = std::max<uint64_t>(total, 1) * 8;
         for (int i = 0; i < 2; i++) HIP_TRY(grow_touched(&w->mbuf[i], &w->mbuf_bytes[i], bytes, s));
         HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->msplit), &w->msplit_bytes,
@@ -1164,16 +1216,15 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
             HIP_TRY(hipStreamSynchronize(s));
             kept = cnt;
         }
-        dout = dst;
+        if (f) {
+            int rc = set_batch_run_locked(f, dst, (size_t)kept, 8, 1, s);
+            if (rc) return rc;
+        }
+        if (!out_on_device && kept)
+            HIP_TRY(hipMemcpyAsync(out_entries, dst, kept * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
     }
     *n_out = (size_t)kept;
-    if (f) {
-        int rc = bloomhip_set_batch_run(f, dout, (size_t)kept, 8, 1, stream);
-        if (rc) return rc;
-    }
-    if (!out_on_device && kept)
-        HIP_TRY(hipMemcpyAsync(out_entries, dout, kept * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
     return BLOOMHIP_OK;
 }
 

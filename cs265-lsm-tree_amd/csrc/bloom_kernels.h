@@ -158,6 +158,11 @@ hipError_t launch_probe_lds(const KeySpan &keys, const ModParams &mp, const uint
                             uint64_t *out, size_t nw_out, hipStream_t stream);
 hipError_t launch_probe(const KeySpan &keys, const ProbeTable &t, uint64_t *out, size_t nwords_out,
                         hipStream_t stream);
+// Scalar set / is_set of one key passed by value (one lane); is_set writes 0/1
+// to *hit (a mapped host word or device memory).
+hipError_t launch_set1(uint32_t *words, const ModParams &mp, int32_t key, hipStream_t stream);
+hipError_t launch_is_set1(const uint32_t *words, const ModParams &mp, int32_t key, uint32_t *hit,
+                          hipStream_t stream);
 // meta[0] = max key, meta[1 ..] = the ceil(n / kFenceStride) fences of a run.
 hipError_t launch_run_meta(const KeySpan &keys, int32_t *meta, hipStream_t stream);
 // Applies the range checks to the probe rows `cand` in place and writes the

@@ -1060,6 +1060,23 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
     }
 }
 
+// Scalar set / is_set (bloomhip_set / bloomhip_is_set): the key is a kernel
+// argument and lane 0 does the reference's work for it
+// (src/bloom_filter.cpp:49-53 / :55-59, all three bits read).
+__global__ void __launch_bounds__(64) k_set1(uint32_t *__restrict__ words, ModParams mp,
+                                             int32_t k) {
+    if (threadIdx.x == 0) set3_global(words, k, mp);
+}
+
+__global__ void __launch_bounds__(64) k_is_set1(const uint32_t *__restrict__ words, ModParams mp,
+                                                int32_t k, uint32_t *__restrict__ hit) {
+    if (threadIdx.x != 0) return;
+    const uint64_t p1 = mod_any(raw_hash1(k), mp), p2 = mod_any(raw_hash2(k), mp),
+                   p3 = mod_any(raw_hash3(k), mp);
+    *hit = (words[p1 >> 5] >> (p1 & 31)) & (words[p2 >> 5] >> (p2 & 31)) &
+           (words[p3 >> 5] >> (p3 & 31)) & 1u;
+}
+
 // Persistent pass-1 grid: two 64-KiB-LDS workgroups per CU for 4096-key
 // tiles, one 112-KiB workgroup for 8192-key tiles.
 inline unsigned part_bin_grid(size_t ntiles, int tb = kPartBlock) {
@@ -1469,6 +1486,17 @@ hipError_t launch_route(const KeySpan &ks, const RouteTable &t, uint64_t *cand, 
     }
 #undef ROUTE_NR
 #undef ROUTE_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_set1(uint32_t *words, const ModParams &mp, int32_t key, hipStream_t stream) {
+    k_set1<<<1, 64, 0, stream>>>(words, mp, key);
+    return hipGetLastError();
+}
+
+hipError_t launch_is_set1(const uint32_t *words, const ModParams &mp, int32_t key, uint32_t *hit,
+                          hipStream_t stream) {
+    k_is_set1<<<1, 64, 0, stream>>>(words, mp, key, hit);
     return hipGetLastError();
 }
 

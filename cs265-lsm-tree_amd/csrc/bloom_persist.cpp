@@ -124,12 +124,22 @@ extern "C" int bloomhip_load(const char *path, int device, bloomhip_filter **out
     std::vector<uint64_t> words;
     std::vector<int32_t> fences;
     uint64_t sum = 0;
-    bool ok = read_all(fp, &h, sizeof h, &fnv) && memcmp(h.magic, kMagic, 8) == 0 &&
-              h.version == kVersion && h.m > 0 && h.nwords == (h.m + 63) / 64 &&
-              h.nwords < (1ull << 58);
+    struct stat st {};
+    // The header is checked against the file's actual size before anything
+    // is sized from it: a damaged or foreign header cannot ask for a huge
+    // allocation.  m is bounded as bloomhip_create bounds it.
+    bool ok = fstat(fileno(fp), &st) == 0 && read_all(fp, &h, sizeof h, &fnv) &&
+              memcmp(h.magic, kMagic, 8) == 0 && h.version == kVersion && h.m > 0 &&
+              h.m <= (1ull << 46) && h.nwords == (h.m + 63) / 64 &&
+              (uint64_t)st.st_size == sizeof(Header) + 8 * h.nwords + 4 * (uint64_t)h.nfences + 8;
     if (ok) {
-        words.resize(h.nwords);
-        fences.resize(h.nfences);
+        try {
+            words.resize(h.nwords);
+            fences.resize(h.nfences);
+        } catch (...) {  // nothing throws across the C ABI
+            fclose(fp);
+            return BLOOMHIP_ENOMEM;
+        }
         ok = read_all(fp, words.data(), words.size() * 8, &fnv) &&
              read_all(fp, fences.data(), fences.size() * 4, &fnv) &&
              read_all(fp, &sum, 8, nullptr) && sum == fnv.h && fgetc(fp) == EOF;

@@ -191,7 +191,14 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
                      int runs_on_device, int drop_tombstones, void *out_entries, size_t *n_out,
                      int out_on_device, bloomhip_filter *f, int device, void *stream);
 
-/* Scalar compatibility entry points (one key; synchronous). */
+/* Scalar compatibility entry points (one key; synchronous), for
+ * BloomFilter::set (src/bloom_filter.cpp:49-53) and is_set (:55-59) called
+ * once per key.  Low-latency path: the key travels as a kernel argument (no
+ * host-to-device copy), one single-lane kernel on HIP's default stream, and
+ * is_set's answer is written straight into a pinned, mapped host word of the
+ * handle: one launch + one stream synchronisation per call (bench.py
+ * `scalar_is_set` measures it).  Calls on one handle serialise on its lock;
+ * batch callers should use bloomhip_set_batch / bloomhip_test_batch. */
 int bloomhip_set(bloomhip_filter *f, int32_t key);
 int bloomhip_is_set(const bloomhip_filter *f, int32_t key, int *hit_out);
 

@@ -1,12 +1,14 @@
 // bloomhip_bloom_filter.hpp — header-only C++ drop-in for the reference's
 // `class BloomFilter` (jackdent/cs265-lsm-tree src/bloom_filter.h:6-15).
 //
-// With the reference's src/bloom_filter.h reduced to
+// With the reference's src/bloom_filter.h reduced to include/dropin/bloom_filter.h
+//     #include <cstdint>
 //     #include "types.h"
 //     #include <bloomhip_bloom_filter.hpp>
 // src/run.cpp compiles unchanged: Run::Run constructs it from
 // `max_size * bf_bits_per_entry` (src/run.cpp:15), Run::put calls set()
 // (src/run.cpp:162) and Run::get calls is_set() (src/run.cpp:93).
+// tests/test_dropin.py compiles the reference's own src/*.cpp this way.
 //
 // set() is buffered on the host and flushed to the GPU as one batch (the
 // reference calls it once per entry of a flush/compaction loop); is_set()
@@ -14,6 +16,10 @@
 // batch methods are the fast path for batched callers.
 #pragma once
 
+// <algorithm> and <cstring>: src/run.cpp uses std::upper_bound (:97, :130,
+// :137) and strdup (:22) without including them; boost/dynamic_bitset.hpp
+// used to bring both in through src/bloom_filter.h.
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <mutex>

@@ -26,8 +26,11 @@
  *   - bitmap layout: boost::dynamic_bitset<unsigned long>, bit i in 64-bit
  *     block i/64 at position i%64, tail bits zero      src/bloom_filter.h:1,7
  */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <math.h>
 
@@ -248,4 +251,110 @@ size_t bo_compact(const int32_t *const *runs, const size_t *n, int nruns, int dr
         }
     }
     return w;
+}
+
+/* ---- CPU baseline on T native threads (bench.py cpu_baseline legs) ---------
+ * The reference's set() loop is sequential per filter (src/run.cpp:159-174)
+ * and its GET search runs one run per pool thread (src/lsm_tree.cpp:180-212).
+ * These give the CPU every core the box has:
+ *   bo_build_mt   ONE filter built by T threads: contiguous key slices, bits
+ *                 set with relaxed atomic ORs into the shared bitmap (OR
+ *                 commutes, so the bitmap is exactly bo_set_batch's);
+ *   bo_build_many nf independent filters, one thread each (per-run builds,
+ *                 as C5 shards runs);
+ *   bo_test_mt    one filter probed by T threads over 64-key-aligned slices. */
+typedef struct {
+    uint64_t *words;
+    const uint64_t *cwords;
+    uint64_t m;
+    const char *keys;
+    size_t lo, hi, stride;
+    uint64_t *packed;
+} bo_task;
+
+static void *bo_build_slice(void *arg) {
+    bo_task *t = (bo_task *)arg;
+    for (size_t i = t->lo; i < t->hi; i++) {
+        int32_t k = bo_key_at(t->keys, i, t->stride);
+        uint64_t p1 = bo_raw1(k) % t->m, p2 = bo_raw2(k) % t->m, p3 = bo_raw3(k) % t->m;
+        __atomic_fetch_or(&t->words[p1 >> 6], 1ull << (p1 & 63), __ATOMIC_RELAXED);
+        __atomic_fetch_or(&t->words[p2 >> 6], 1ull << (p2 & 63), __ATOMIC_RELAXED);
+        __atomic_fetch_or(&t->words[p3 >> 6], 1ull << (p3 & 63), __ATOMIC_RELAXED);
+    }
+    return NULL;
+}
+
+static void *bo_test_slice(void *arg) {
+    bo_task *t = (bo_task *)arg;
+    for (size_t i = t->lo; i < t->hi; i++)
+        if (bo_is_set(t->cwords, t->m, bo_key_at(t->keys, i, t->stride)))
+            t->packed[i >> 6] |= 1ull << (i & 63);  /* slices are 64-key aligned */
+    return NULL;
+}
+
+static int bo_run_threads(bo_task *tasks, int T, void *(*fn)(void *)) {
+    pthread_t *th = (pthread_t *)calloc((size_t)T, sizeof(pthread_t));
+    if (!th) return -BO_EINVAL;
+    int started = 0, rc = 0;
+    for (; started < T; started++)
+        if (pthread_create(&th[started], NULL, fn, &tasks[started]) != 0) { rc = -BO_EINVAL; break; }
+    for (int i = 0; i < started; i++) pthread_join(th[i], NULL);
+    free(th);
+    return rc;
+}
+
+int bo_build_mt(uint64_t *words, uint64_t m, const void *keys, size_t n, size_t stride, int T) {
+    if (m == 0 || T < 1) return -BO_EINVAL;
+    bo_task *tasks = (bo_task *)calloc((size_t)T, sizeof(bo_task));
+    if (!tasks) return -BO_EINVAL;
+    for (int i = 0; i < T; i++) {
+        tasks[i].words = words;
+        tasks[i].m = m;
+        tasks[i].keys = (const char *)keys;
+        tasks[i].stride = stride;
+        tasks[i].lo = n * (size_t)i / (size_t)T;
+        tasks[i].hi = n * (size_t)(i + 1) / (size_t)T;
+    }
+    int rc = bo_run_threads(tasks, T, bo_build_slice);
+    free(tasks);
+    return rc;
+}
+
+/* nf filters: filter f gets keys[f*n .. (f+1)*n) into words + f*ceil(m/64). */
+int bo_build_many(uint64_t *words, uint64_t m, const int32_t *keys, size_t n, int nf) {
+    if (m == 0 || nf < 1) return -BO_EINVAL;
+    bo_task *tasks = (bo_task *)calloc((size_t)nf, sizeof(bo_task));
+    if (!tasks) return -BO_EINVAL;
+    for (int f = 0; f < nf; f++) {
+        tasks[f].words = words + (size_t)f * bo_words(m);
+        tasks[f].m = m;
+        tasks[f].keys = (const char *)(keys + (size_t)f * n);
+        tasks[f].stride = 4;
+        tasks[f].lo = 0;
+        tasks[f].hi = n;
+    }
+    int rc = bo_run_threads(tasks, nf, bo_build_slice);
+    free(tasks);
+    return rc;
+}
+
+int bo_test_mt(const uint64_t *words, uint64_t m, const void *keys, size_t n, size_t stride,
+               uint64_t *packed, int T) {
+    if (m == 0 || T < 1) return -BO_EINVAL;
+    bo_task *tasks = (bo_task *)calloc((size_t)T, sizeof(bo_task));
+    if (!tasks) return -BO_EINVAL;
+    const size_t nw = (n + 63) / 64;
+    for (int i = 0; i < T; i++) {
+        tasks[i].cwords = words;
+        tasks[i].m = m;
+        tasks[i].keys = (const char *)keys;
+        tasks[i].stride = stride;
+        tasks[i].packed = packed;
+        tasks[i].lo = 64 * (nw * (size_t)i / (size_t)T);
+        size_t hi = 64 * (nw * (size_t)(i + 1) / (size_t)T);
+        tasks[i].hi = hi < n ? hi : n;
+    }
+    int rc = bo_run_threads(tasks, T, bo_test_slice);
+    free(tasks);
+    return rc;
 }

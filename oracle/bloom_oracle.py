@@ -151,6 +151,14 @@ class COracle:
         L.bo_route.restype = ctypes.c_int
         L.bo_compact.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P]
         L.bo_compact.restype = ctypes.c_size_t
+        L.bo_build_mt.argtypes = [P, ctypes.c_uint64, P, ctypes.c_size_t, ctypes.c_size_t,
+                                  ctypes.c_int]
+        L.bo_build_mt.restype = ctypes.c_int
+        L.bo_build_many.argtypes = [P, ctypes.c_uint64, P, ctypes.c_size_t, ctypes.c_int]
+        L.bo_build_many.restype = ctypes.c_int
+        L.bo_test_mt.argtypes = [P, ctypes.c_uint64, P, ctypes.c_size_t, ctypes.c_size_t, P,
+                                 ctypes.c_int]
+        L.bo_test_mt.restype = ctypes.c_int
         self.L = L
 
     def m_bits(self, max_size: int, bpe: float) -> int:
@@ -199,6 +207,35 @@ class COracle:
         rc = self.L.bo_test_batch(w.ctypes.data, m, buf.ctypes.data, n, stride, out.ctypes.data)
         if rc != 0:
             raise ValueError(f"bo_test_batch rc={rc}")
+        return out
+
+    def build_mt(self, m: int, keys, threads: int) -> np.ndarray:
+        """build() on `threads` native threads (one shared bitmap, atomic ORs)."""
+        buf = np.ascontiguousarray(keys, dtype=np.int32)
+        words = np.zeros(np_words(m), dtype=np.uint64)
+        rc = self.L.bo_build_mt(words.ctypes.data, m, buf.ctypes.data, buf.size, 4, threads)
+        if rc != 0:
+            raise ValueError(f"bo_build_mt rc={rc}")
+        return words
+
+    def build_many(self, m: int, keys_2d) -> np.ndarray:
+        """One filter per row of keys_2d, one native thread each."""
+        k = np.ascontiguousarray(keys_2d, dtype=np.int32)
+        words = np.zeros((k.shape[0], np_words(m)), dtype=np.uint64)
+        rc = self.L.bo_build_many(words.ctypes.data, m, k.ctypes.data, k.shape[1], k.shape[0])
+        if rc != 0:
+            raise ValueError(f"bo_build_many rc={rc}")
+        return words
+
+    def test_mt(self, words: np.ndarray, m: int, keys, threads: int) -> np.ndarray:
+        """test() on `threads` native threads."""
+        buf = np.ascontiguousarray(keys, dtype=np.int32)
+        out = np.zeros((buf.size + 63) // 64, dtype=np.uint64)
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        rc = self.L.bo_test_mt(w.ctypes.data, m, buf.ctypes.data, buf.size, 4, out.ctypes.data,
+                               threads)
+        if rc != 0:
+            raise ValueError(f"bo_test_mt rc={rc}")
         return out
 
     def popcount(self, words: np.ndarray) -> int:

@@ -157,3 +157,42 @@ def test_load_of_a_non_filter_file_fails_before_touching_the_gpu(tmp_path):
     assert L.bloomhip_load(str(p).encode(), 0, ctypes.byref(h)) == bh.EINVAL
     assert L.bloomhip_load(str(tmp_path / "none").encode(), 0, ctypes.byref(h)) == -5  # EIO
     assert not h.value
+
+
+def test_load_rejects_oversized_header_without_allocating(tmp_path):
+    """A header whose sizes disagree with the file (here: 2^46 bits and 2^32-1
+    fences in a 48-byte file) is refused before anything is sized from it."""
+    import ctypes
+    import struct
+    L = bh._lib()
+    h = ctypes.c_void_p()
+    for m, nf in [((1 << 46), 0xFFFFFFFF), ((1 << 62), 0), (1000, 5)]:
+        hdr = b"BLOOMHP1" + struct.pack("<IIQQIi", 1, 1, m, (m + 63) // 64, nf, 0)
+        p = tmp_path / f"big_{m}_{nf}.bloom"
+        p.write_bytes(hdr + b"\0" * 8)
+        assert L.bloomhip_load(str(p).encode(), 0, ctypes.byref(h)) == bh.EINVAL
+        assert not h.value
+
+
+def test_binding_refuses_keys_that_are_not_int32():
+    """Keys are KEY_t = int32 (src/types.h:4): an int64 array read as int32
+    words would build the wrong keys, so the binding converts integer arrays
+    at stride 4 (when they fit) and refuses anything else."""
+    ptr, on_dev, keep = bh._keys_ptr(np.arange(10), 4)  # numpy's default int64
+    assert keep.dtype == np.int32 and list(keep) == list(range(10)) and on_dev == 0
+    with pytest.raises(ValueError):
+        bh._keys_ptr(np.array([2**31]), 4)          # out of range
+    with pytest.raises(ValueError):
+        bh._keys_ptr(np.zeros((4, 2), dtype=np.int64), 8)  # int64 entries at stride 8
+    with pytest.raises(ValueError):
+        bh._keys_ptr(np.zeros(4, dtype=np.float32), 4)
+    _, _, keep = bh._keys_ptr(np.zeros(8, dtype=np.int32), 8)
+    assert bh._key_count(keep, 8, None) == 4
+    with pytest.raises(ValueError):
+        bh._key_count(keep, 8, 5)                  # 5 keys at stride 8 need 36 bytes
+    with pytest.raises(ValueError):
+        bh._out_ptr(np.zeros(3, dtype=np.uint64), 32, 8, "out")   # too small
+    with pytest.raises(ValueError):
+        bh._out_ptr(np.zeros(8, dtype=np.int32), 16, 8, "out")    # wrong element size
+    with pytest.raises(ValueError):
+        bh.compact([np.zeros((4, 2), dtype=np.int64)])

@@ -159,3 +159,18 @@ def test_compact_restatement_matches_python(coracle):
                 if not (drop and v == np.iinfo(np.int32).min)]
         got = coracle.compact(runs, drop)
         assert [tuple(x) for x in got.tolist()] == want
+
+
+def test_threaded_oracle_entries_match_sequential(coracle):
+    """bench.py's CPU baseline at T threads computes exactly the sequential
+    restatement's bitmap and hits (the OR of bits commutes)."""
+    rng = np.random.default_rng(11)
+    keys = rng.integers(-2**31, 2**31, size=300_007, dtype=np.int64).astype(np.int32)
+    m = 2_000_003
+    want = coracle.build(m, keys)
+    for T in (1, 3, 16):
+        assert (coracle.build_mt(m, keys, T) == want).all()
+        assert (coracle.test_mt(want, m, keys[:70_001], T) == coracle.test(want, m, keys[:70_001])).all()
+    many = coracle.build_many(m, keys[:300_000].reshape(3, -1))
+    for f in range(3):
+        assert (many[f] == coracle.build(m, keys[f * 100_000:(f + 1) * 100_000])).all()

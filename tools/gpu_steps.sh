@@ -1,0 +1,42 @@
+#!/bin/bash
+# Runs named GPU steps in order on the box, each under its own time limit,
+# stopping at the first failure (no retries).  Logs: gpurun_out/<tag>/<step>.log
+# Usage: tools/gpu_steps.sh TAG step[,step...]
+#   steps: pytest smoke bench bench_c4 bench_c5 stats_c2 stats_c3 pmc_c2 pmc_c4 pmc_c5
+set -o pipefail
+TAG=${1:?tag}; STEPS=${2:?steps}
+OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"; grep -v amdgpu.ids "$OUT/$name.log" | tail -${TAILN:-3} | cut -c1-400
+  return $rc
+}
+pmc() {  # workload counter benchargs...
+  local w=$1 c=$2; shift 2
+  run "pmc_${w}_$c" 150 timeout -s KILL 140 rocprofv3 --pmc "$c" --kernel-trace \
+      -d "$OUT/pmc_${w}_$c" -o pmc --output-format csv -- python bench.py "$@"
+}
+for s in ${STEPS//,/ }; do
+  case $s in
+    pytest) run pytest 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    bench) run bench 600 python bench.py || exit 1 ;;
+    bench_quick) run bench_quick 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline || exit 1 ;;
+    bench_c4) run bench_c4 400 python bench.py --workload c4 --steps 5 --warmup 1 --no-extras --no-cpu-baseline || exit 1 ;;
+    bench_c5) run bench_c5 400 python bench.py --workload c5 --steps 20 --warmup 3 --no-extras --no-cpu-baseline || exit 1 ;;
+    stats_c2) run stats_c2 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c2" -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline --prewarm-s 0 || exit 1 ;;
+    stats_c3) run stats_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3" -o run --output-format csv -- python tools/probe_prof.py auto 30 || exit 1 ;;
+    pmc_c2) pmc c2 FETCH_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
+            pmc c2 WRITE_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
+    pmc_c4) pmc c4 FETCH_SIZE --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
+            pmc c4 WRITE_SIZE --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
+    pmc_c5) pmc c5 FETCH_SIZE --workload c5 --steps 5 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
+            pmc c5 WRITE_SIZE --workload c5 --steps 5 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "all steps ok"
