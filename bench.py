@@ -34,6 +34,8 @@ WORKLOADS = {
     "c2": (16_777_216, 10.0),
     "c5": (67_108_864, 10.0),
     "c4": (268_435_456, 12.0),
+    # a run whose filter needs 64-bit positions: m = 2^32 bits (512 MiB)
+    "c4w": (268_435_456, 16.0),
 }
 BUILD_SLOTS = ("k_build_atomic", "k_build_lds", "k_part_bin", "k_part_apply",
                "part_counts(memset)")

@@ -184,7 +184,7 @@ hipError_t grow_touched(void **ptr, size_t *have, size_t need, hipStream_t s) {
 // output run's filter, which takes it again (run_partition).
 struct Workspace {
     std::recursive_mutex mu;  // held while work using the buffers is enqueued
-    uint32_t *pos = nullptr;  // tile-sorted segment offsets
+    uint64_t *pos = nullptr;  // tile-sorted packed entries
     size_t pos_bytes = 0;
     uint32_t *runs = nullptr;  // run starts: tile-major rows, then segment-major
     size_t runs_bytes = 0;
@@ -284,18 +284,17 @@ int device_keys(bloomhip_filter *f, const void *keys, size_t n, size_t stride, i
 
 bool partition_able(const bloomhip_filter *f) {
     PartitionWorkspace ws{};
-    return f->mp.fast && plan_segments(f->m, device_cu_count(), &ws);
+    return plan_segments(f->m, device_cu_count(), &ws);
 }
 
 int resolve_strategy(const bloomhip_filter *f, size_t n) {
     if (f->strategy != BLOOMHIP_BUILD_AUTO) return f->strategy;
-    if (!f->mp.fast) return BLOOMHIP_BUILD_ATOMIC;
     const uint64_t bytes = (f->m + 7) / 8;
     if (bytes <= kLdsBitmapBytes) {
         // Worth a private LDS copy once the batch outweighs the merge.
         return n >= (size_t)(f->m / 64) ? BLOOMHIP_BUILD_LDS : BLOOMHIP_BUILD_ATOMIC;
     }
-    // The partition build pays two passes over 12 B/key; below ~64K keys a
+    // The partition build pays two passes over 8 B/key; below ~64K keys a
     // direct atomic build is cheaper.
     if (n >= (1u << 16) && partition_able(f)) return BLOOMHIP_BUILD_PARTITION;
     return BLOOMHIP_BUILD_ATOMIC;
@@ -317,7 +316,7 @@ int partition_buffers(Workspace *w, size_t n, hipStream_t s, PartitionWorkspace 
     if (ws.tile_keys == 0) ws.tile_keys = choose_tile_keys(ws.nbins);
     ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->pos), &w->pos_bytes,
-                         ws.ntiles * (size_t)ws.tile_keys * 3 * 4, s));
+                         ws.ntiles * (size_t)ws.tile_keys * 8, s));
     const size_t table = ws.ntiles * (ws.nbins + 1);  // run starts, both layouts
     HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->runs), &w->runs_bytes, table * 2 * 4, s));
     ws.pos = w->pos;

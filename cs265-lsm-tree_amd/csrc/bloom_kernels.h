@@ -52,13 +52,12 @@ struct RouteTable {
 // CU on gfx950, one such workgroup per CU.
 constexpr size_t kLdsBitmapBytes = 160 * 1024;
 
-// Partition build geometry.  Pass 1 counting-sorts positions by sub-segment
-// p >> sub_shift (nsub <= kPartMaxBins sub-segments of 2^sub_shift bits).
-// Pass 2 gives each workgroup g consecutive sub-segments = one segment of
-// S = g << sub_shift bits (S <= 160 KiB, so it fits one workgroup's LDS);
-// their runs are adjacent in every sorted tile, so a workgroup still reads one
-// contiguous run per tile.  plan_segments picks (sub_shift, g) so the number
-// of segments is a multiple of the CU count: every CU of pass 2 gets the same
+// Partition build geometry.  Pass 1 counting-sorts a tile's 3 positions per
+// key by SEGMENT (b = p / S, S = seg_bits <= 160 KiB of bits, so a segment
+// fits one workgroup's LDS), computed as (p >> sub_shift) / group with a
+// host-verified multiply-high (SegMap).  Pass 2 gives each segment to one
+// workgroup.  plan_segments picks (sub_shift, group) so that the number of
+// segments is a multiple of the CU count: every CU of pass 2 gets the same
 // share.
 constexpr uint32_t kSegMaxBits = 144u * 1024u * 8u;  // 144 KiB of LDS (stacked-probe planes)
 // Pass 2 has no static LDS: segment images may use all 160 KiB (plan_segments).
@@ -67,7 +66,71 @@ constexpr int kPartBlock = 512;
 constexpr int kPartKPT = 8;  // keys per thread in pass 1
 constexpr size_t kPartTileKeys = (size_t)kPartBlock * kPartKPT;  // 4096
 constexpr int kPartTilePos = (int)kPartTileKeys * 3;
-constexpr size_t kPartMaxBins = 4096;  // sub-segments sorted by pass 1
+constexpr size_t kPartMaxBins = 4096;     // segments of a 4096-key tile (512 threads)
+constexpr size_t kPartMaxBinsBig = 8192;  // segments of an 8192-key tile (1024 threads)
+constexpr size_t kPartMaxSub = 8192;      // p >> sub_shift below this (SegMap's domain)
+
+// Sorted-tile entries: the low kEntryBits bits of each position, three per
+// u64 (bits 0-20, 21-41, 42-62).  A segment has at most kStackMaxBits <
+// 2^21 bits, so within segment b's run (known by index from the run table)
+// the offset is exactly (entry - b*S) mod 2^21.  8 B per 3 entries instead of
+// 12, and the same format for any m (2^46 included).
+constexpr uint32_t kEntryBits = 21;
+constexpr uint32_t kEntryMask = (1u << kEntryBits) - 1u;
+static_assert(kStackMaxBits <= (1u << kEntryBits), "segment offsets fit an entry");
+
+// p -> segment: q = p >> shift (< kPartMaxSub), b = ident ? q : mulhi(q, magic).
+struct SegMap {
+    uint32_t shift;
+    uint32_t magic;  // ceil(2^32 / group), checked exact for every q < nsub
+    uint32_t ident;  // group == 1
+    uint32_t nbins;
+};
+
+struct PartitionWorkspace {
+    uint64_t *pos;         // [ntiles * tile_keys] packed sorted entries (3 per u64)
+    uint32_t *run_rows;    // [ntiles * (nbins + 1)], pass-1 run starts, tile-major
+    uint32_t *run_starts;  // [(nbins + 1) * ntiles], the same segment-major (pass 2)
+    size_t ntiles;
+    size_t nbins;          // segments
+    uint32_t sub_shift;    // q = pos >> sub_shift
+    uint32_t group;        // q's per segment
+    uint32_t nsub;         // number of q values
+    uint32_t seg_bits;     // S = group << sub_shift
+    uint32_t tile_keys;    // keys per pass-1 tile: kPartTileKeys, or twice that (0 = default)
+    uint32_t magic;        // SegMap::magic
+};
+
+inline SegMap seg_map_of(const PartitionWorkspace &ws) {
+    return SegMap{ws.sub_shift, ws.magic, ws.group == 1 ? 1u : 0u, (uint32_t)ws.nbins};
+}
+
+// Keys per pass-1 tile for a batch sorted into nbins segments: short runs
+// make pass 2 line-bound, so batches with more than 256 segments (under 48
+// entries per segment of a 4096-key tile) sort 8192-key tiles (one
+// 1024-thread workgroup per CU) and get runs twice as long: C3, C4 and C5,
+// while C2's 256 segments keep 4096-key tiles.  More than kPartMaxBins
+// segments always need the 8192-key tile (its histogram holds 8192).
+inline uint32_t choose_tile_keys(size_t nbins) {
+    return nbins > 256 ? 2 * (uint32_t)kPartTileKeys : (uint32_t)kPartTileKeys;
+}
+inline size_t tile_keys_of(const PartitionWorkspace &ws) {
+    return ws.tile_keys ? ws.tile_keys : kPartTileKeys;
+}
+
+// Geometry of a stacked probe (seg_bits = w): false when no w = g << s with
+// w | m_max, w <= m_min (the smallest member), nf * w bits <= kStackMaxBits
+// and <= kPartMaxBins segments exists.  Prefers the widest w that still
+// gives >= ncu segments.  gcd_m: gcd of the members' sizes (a multiple of
+// 128 bits).
+bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
+                PartitionWorkspace *ws);
+
+// CUs of the current device (cached).
+int device_cu_count();
+// Fills the geometry fields of ws for a filter of m bits; false when the
+// partition path does not apply (m > kPartMaxSub * 2^20 = 2^33 bits).
+bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws);
 
 // Probe: filters up to this size are gathered directly; larger ones use the
 // partitioned probe when the batch has at least kProbePartitionMinKeys keys.
@@ -97,50 +160,6 @@ struct StackTable {
     int nf;
 };
 
-struct PartitionWorkspace {
-    uint32_t *pos;         // [ntiles * kPartTilePos] tile-sorted positions
-    uint32_t *run_rows;    // [ntiles * (nbins + 1)], pass-1 run starts, tile-major
-    uint32_t *run_starts;  // [(nbins + 1) * ntiles], the same segment-major (pass 2)
-    size_t ntiles;
-    size_t nbins;          // pass-2 segments
-    uint32_t sub_shift;    // pass-1 sub-segment = pos >> sub_shift
-    uint32_t group;        // sub-segments per pass-2 segment
-    uint32_t nsub;         // pass-1 sub-segments
-    uint32_t seg_bits;     // S = group << sub_shift
-    uint32_t tile_keys;    // keys per pass-1 tile: kPartTileKeys, or twice that (0 = default)
-};
-
-// Keys per pass-1 tile for a batch sorted into nbins segments: short runs
-// make pass 2 line-bound, so batches with more than 256 segments (under 48
-// entries per segment of a 4096-key tile) sort 8192-key tiles (one
-// 1024-thread workgroup per CU) and get runs twice as long: C3, C4 and C5
-// (C5: pass 2 0.302 -> 0.263 ms with 512 segments), while C2's 256 segments
-// keep 4096-key tiles (8192 cost C2 125 -> 112 Gkeys/s).
-// BLOOMHIP_BIG_TILE_BINS overrides the threshold (tuning experiments).
-inline uint32_t choose_tile_keys(size_t nbins) {
-    static const size_t threshold = [] {
-        const char *e = getenv("BLOOMHIP_BIG_TILE_BINS");
-        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)256;
-    }();
-    return nbins > threshold ? 2 * (uint32_t)kPartTileKeys : (uint32_t)kPartTileKeys;
-}
-inline size_t tile_keys_of(const PartitionWorkspace &ws) {
-    return ws.tile_keys ? ws.tile_keys : kPartTileKeys;
-}
-
-// Geometry of a stacked probe (seg_bits = w): false when no w = g << s with
-// w | m_max, w <= m_min (the smallest member), nf * w bits <= kStackMaxBits
-// and <= kPartMaxBins sub-segments exists.  Prefers the widest w that still
-// gives >= ncu segments.  gcd_m: gcd of the members' sizes (a multiple of
-// 128 bits).
-bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
-                PartitionWorkspace *ws);
-
-// CUs of the current device (cached).
-int device_cu_count();
-// Fills the geometry fields of ws for a filter of m bits; false when the
-// partition path does not apply (m >= 2^32).
-bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws);
 
 // Kernels enqueued on `stream`; all return hipSuccess or the launch error.
 hipError_t launch_build_atomic(const KeySpan &keys, const ModParams &mp, uint32_t *words,
@@ -169,7 +188,7 @@ hipError_t launch_run_meta(const KeySpan &keys, int32_t *meta, hipStream_t strea
 // newest candidate run and its page index per key (first/page may be null).
 hipError_t launch_route(const KeySpan &keys, const RouteTable &t, uint64_t *cand, size_t nw,
                         int32_t *first, int32_t *page, hipStream_t stream);
-// Partitioned probe of one filter (fast mod, nbins <= kPartMaxBins): bin the
+// Partitioned probe of one filter (nbins as plan_segments): bin the
 // keys' positions by segment (recording each position's sorted slot), test
 // each segment in LDS writing one result byte per sorted entry, then AND each
 // key's three bytes into out[ceil(n/64)].  Workspace: res holds

@@ -53,9 +53,9 @@ __device__ __forceinline__ void set3_global(uint32_t *words, int32_t k, const Mo
         global_or(words, pos32(raw_hash2(k), mp));
         global_or(words, pos32(raw_hash3(k), mp));
     } else {
-        global_or(words, raw_hash1(k) % mp.m);
-        global_or(words, raw_hash2(k) % mp.m);
-        global_or(words, raw_hash3(k) % mp.m);
+        global_or(words, mod_wide(raw_hash1(k), mp));
+        global_or(words, mod_wide(raw_hash2(k), mp));
+        global_or(words, mod_wide(raw_hash3(k), mp));
     }
 }
 
@@ -123,23 +123,24 @@ __global__ void __launch_bounds__(kBlock) k_build_lds(KeySpan ks, ModParams mp,
 }
 
 // ---------------------------------------------------------------------------
-// partition pass 1 (k_part_bin): persistent 512-thread workgroups walk tiles
-// of kPartTileKeys keys.  Each thread hashes kPartKPT keys; the 3 positions
-// are counting-sorted by sub-segment (pos >> sub_shift) in LDS and the sorted
-// tile (full positions) is written contiguously to pos_out[tile*kPartTilePos..].
-// Row `tile` of run_starts holds, for each pass-2 segment b (= sub-segments
-// [b*group, (b+1)*group)), where its run of this tile starts (nbins + 1
-// entries), so segment b's run is [run_starts[tile][b], run_starts[tile][b+1]).
-// No global atomics.
+// partition pass 1 (k_part_bin): persistent workgroups of TB threads walk
+// tiles of TB * kPartKPT keys.  Each thread hashes kPartKPT keys; the tile's
+// 3 positions per key are counting-sorted by segment in LDS (an LDS atomic
+// gives each its rank in its segment, a scan gives the segment offsets) and
+// the sorted tile goes out packed: the low kEntryBits bits of each position,
+// three per u64, 8 B per key-hash triple instead of 12.
+// Column `tile` of the segment-major run table gets where each segment's run
+// starts (nbins + 1 entries), so segment b's run of this tile is
+// [runs[b][tile], runs[b+1][tile]).  No global atomics.
 //
 // The next tile's keys are loaded while the current tile is sorted, and the
 // workgroup barriers wait only for LDS (lgkmcnt), so the sorted tile's
 // stores drain under the next tile's hashing.
 //
+// WIDE: m >= 2^32 (64-bit positions, mod_wide); the entries are the same.
 // SLOTS (partitioned probe): also write, per key and hash, the index its
-// position got in the sorted tile: slots[(tile*3 + h)*kPartTileKeys + key].
+// position got in the sorted tile: slots[(tile*3 + h)*tile_keys + key].
 // ---------------------------------------------------------------------------
-constexpr int kMaxBins = (int)kPartMaxBins;
 
 // Workgroup barrier that waits for this wave's LDS operations only.
 __device__ __forceinline__ void lds_barrier() {
@@ -189,33 +190,42 @@ __device__ __forceinline__ size_t part_tile(size_t k, size_t ntiles) {
     return blockIdx.x < nr ? base + xcd_remap(blockIdx.x, (unsigned)nr) : ntiles;
 }
 
-// ABLATE (timing builds only, tools/ubench): 1 = skip the sorted-tile store,
-// 2 = also skip the LDS scatter, 3 = hash only.  The product launches 0.
-// Outputs: pos_out[tile * kPartTilePos + i], the tile's positions sorted by
-// sub-segment, and where segment b's run of the tile starts (b = 0..nbins):
-// COLS = true: straight into the segment-major table runs[b * ntiles + tile];
-// COLS = false: into the tile-major runs[tile * (nbins + 1) + b], for
-// k_runs_transpose (large tables: see there).
-template <int LAYOUT, int ABLATE = 0, bool SLOTS = false, bool COLS = true, int TB = kPartBlock,
-          int STAGGER = 0>
+// The segment of position p (SegMap: a shift, then an exact multiply-high
+// division by the group, checked on the host for every shifted value).
+template <typename P>
+__device__ __forceinline__ uint32_t seg_of(P p, const SegMap &sm) {
+    const uint32_t q = (uint32_t)(p >> sm.shift);
+    return sm.ident ? q : __umulhi(q, sm.magic);
+}
+
+// Rank bits of a (segment, rank) register: ranks < 3 * 8192 < 2^15.
+constexpr uint32_t kRankBits = 15;
+
+// Outputs: pos_out[tile * kTileKeys ..] (u64), the tile's entries sorted by
+// segment, packed three per u64; where segment b's run of the tile starts
+// (b = 0..nbins): COLS = true: straight into the segment-major table
+// runs[b * ntiles + tile]; COLS = false: into the tile-major
+// runs[tile * (nbins + 1) + b], for k_runs_transpose (large tables).
+template <int LAYOUT, bool SLOTS, bool COLS, int TB, bool WIDE>
 __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
-                                                         uint32_t *__restrict__ pos_out,
-                                                         uint32_t *__restrict__ runs,
-                                                         int nbins, int nsub, int sub_shift,
-                                                         int group, size_t ntiles,
-                                                         uint16_t *__restrict__ slots) {
-    // tile = TB * kPartKPT keys
+                                                    uint64_t *__restrict__ pos_out,
+                                                    uint32_t *__restrict__ runs, SegMap sm,
+                                                    size_t ntiles, uint16_t *__restrict__ slots) {
     constexpr int kTileKeys = TB * kPartKPT;
     constexpr int kTilePos = 3 * kTileKeys;
-    constexpr int kScanPer = (kMaxBins + 1 + TB - 1) / TB;  // scan entries per thread
+    constexpr int kMaxB = TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
+    constexpr int kScanPer = (kMaxB + 1 + TB - 1) / TB;  // scan entries per thread, at most
+    static_assert(kTilePos < (1 << kRankBits), "ranks fit their field");
     // static LDS even for the 96 KiB of an 8192-key tile (gfx950 takes it);
     // dynamic LDS or a pointer to it made the compiler spill registers here
     __shared__ __attribute__((aligned(16))) uint32_t s_sorted[kTilePos];
-    __shared__ uint32_t s_hist[kMaxBins + 1];
+    __shared__ uint32_t s_hist[kMaxB + 1];
     __shared__ uint32_t s_wsum[TB / 64];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
+    const int nb = (int)sm.nbins;
+    const int per = (nb + 1 + TB - 1) / TB;  // this launch's scan entries per thread
     int32_t kcur[kPartKPT], knext[kPartKPT];
 
     // One tile.  FULL (every tile but a short last one) makes the key count a
@@ -228,50 +238,48 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
         const size_t tile0 = tile * kTileKeys;
         const int tile_keys = FULL ? (int)kTileKeys : (int)min((size_t)kTileKeys, ks.n - tile0);
         auto live = [&](int j) { return FULL || j * TB + tid < tile_keys; };
-        for (int b = tid; b <= nsub; b += TB) s_hist[b] = 0;
+        for (int b = tid; b <= nb; b += TB) s_hist[b] = 0;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
 
-        // 1. positions, and each one's rank inside its sub-segment (LDS
-        //    atomics).  The ranks are not consumed before the barrier, so all
-        //    24 atomics of a thread stay in flight behind the hashing.
-        uint32_t pos[kPartKPT * 3];
-        uint32_t rank[kPartKPT * 3];
+        // 1. positions -> (segment, rank in segment) and the entry; the ranks
+        //    are not consumed before the barrier, so all 24 LDS atomics of a
+        //    thread stay in flight behind the hashing.
+        uint32_t br[kPartKPT * 3];   // segment << kRankBits | rank
+        uint32_t ent[kPartKPT * 3];  // low kEntryBits bits of the position
 #pragma unroll
         for (int j = 0; j < kPartKPT; j++) {
             if (live(j)) {
                 const int32_t k = kcur[j];
-                pos[3 * j + 0] = pos32(raw_hash1(k), mp);
-                pos[3 * j + 1] = pos32(raw_hash2(k), mp);
-                pos[3 * j + 2] = pos32(raw_hash3(k), mp);
-                if constexpr (ABLATE < 3) {
 #pragma unroll
-                    for (int h = 0; h < 3; h++)
-                        rank[3 * j + h] = atomicAdd(&s_hist[pos[3 * j + h] >> sub_shift], 1u);
+                for (int h = 0; h < 3; h++) {
+                    const uint64_t raw = h == 0 ? raw_hash1(k) : h == 1 ? raw_hash2(k) : raw_hash3(k);
+                    uint32_t b;
+                    if constexpr (WIDE) {
+                        const uint64_t p = mod_wide(raw, mp);
+                        b = seg_of(p, sm);
+                        ent[3 * j + h] = (uint32_t)p & kEntryMask;
+                    } else {
+                        const uint32_t p = mod_fast(raw, mp);
+                        b = seg_of(p, sm);
+                        ent[3 * j + h] = p & kEntryMask;
+                    }
+                    br[3 * j + h] = (b << kRankBits) | atomicAdd(&s_hist[b], 1u);
                 }
             } else {
 #pragma unroll
-                for (int h = 0; h < 3; h++) pos[3 * j + h] = rank[3 * j + h] = 0;
+                for (int h = 0; h < 3; h++) br[3 * j + h] = ent[3 * j + h] = 0;
             }
-        }
-        if constexpr (ABLATE == 3) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int j = 0; j < kPartKPT * 3; j++) acc ^= pos[j];
-            if (acc == 0x9E3779B9u) pos_out[tid] = acc;
-            if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
-            return;
         }
         lds_barrier();
 
-        // 2. exclusive scan of the nsub+1 counts (the extra slot is 0 and
-        //    receives the tile total); the run of pass-2 segment b starts at
-        //    sub-segment b*group.
+        // 2. exclusive scan of the nbins+1 counts (the extra slot is 0 and
+        //    receives the tile total); thread t owns [t*per, t*per + per).
         uint32_t local[kScanPer];
         uint32_t tsum = 0;
 #pragma unroll
         for (int q = 0; q < kScanPer; q++) {
-            const int b = tid * kScanPer + q;
-            local[q] = b <= nsub ? s_hist[b] : 0u;
+            const int b = tid * per + q;
+            local[q] = (q < per && b <= nb) ? s_hist[b] : 0u;
             tsum += local[q];
         }
         uint32_t incl = tsum;
@@ -286,80 +294,69 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
         for (int w = 0; w < wave; w++) run += s_wsum[w];
 #pragma unroll
         for (int q = 0; q < kScanPer; q++) {
-            const int b = tid * kScanPer + q;
-            if (b <= nsub) {
+            const int b = tid * per + q;
+            if (q < per && b <= nb) {
                 s_hist[b] = run;
                 run += local[q];
             }
         }
         lds_barrier();
         if constexpr (COLS) {
-            for (int b = tid; b <= nbins; b += TB)
-                runs[(size_t)b * ntiles + tile] = s_hist[b == nbins ? nsub : b * group];
+            for (int b = tid; b <= nb; b += TB) runs[(size_t)b * ntiles + tile] = s_hist[b];
         } else {
-            uint32_t *row = runs + tile * (size_t)(nbins + 1);
-            for (int b = tid; b <= nbins; b += TB)
-                row[b] = s_hist[b == nbins ? nsub : b * group];
+            uint32_t *row = runs + tile * (size_t)(nb + 1);
+            for (int b = tid; b <= nb; b += TB) row[b] = s_hist[b];
         }
         if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
 
-        if constexpr (ABLATE < 2) {
-            // 3. scatter into the LDS image sorted by sub-segment: all 24
-            //    bin-offset reads first (one wait), then the writes.
-            uint32_t slot[kPartKPT * 3];
+        // 3. scatter into the LDS image sorted by segment, one hash at a time:
+        //    its kPartKPT offset reads first (one wait), then the writes.
 #pragma unroll
-            for (int q = 0; q < kPartKPT * 3; q++) slot[q] = s_hist[pos[q] >> sub_shift] + rank[q];
+        for (int h = 0; h < 3; h++) {
+            uint32_t slot[kPartKPT];
+#pragma unroll
+            for (int j = 0; j < kPartKPT; j++)
+                slot[j] = s_hist[br[3 * j + h] >> kRankBits] +
+                          (br[3 * j + h] & ((1u << kRankBits) - 1u));
 #pragma unroll
             for (int j = 0; j < kPartKPT; j++) {
                 if (live(j)) {
-#pragma unroll
-                    for (int h = 0; h < 3; h++) {
-                        s_sorted[slot[3 * j + h]] = pos[3 * j + h];  // full position
-                        if constexpr (SLOTS)
-                            slots[(tile * 3 + h) * kTileKeys + j * TB + tid] =
-                                (uint16_t)slot[3 * j + h];
-                    }
+                    s_sorted[slot[j]] = ent[3 * j + h];
+                    if constexpr (SLOTS)
+                        slots[(tile * 3 + h) * kTileKeys + j * TB + tid] = (uint16_t)slot[j];
                 }
             }
-            lds_barrier();
         }
+        lds_barrier();
 
-        if constexpr (ABLATE == 0) {
-            // 4. the sorted tile goes out with 16-byte stores.
-            uint32_t *dst = pos_out + tile * (size_t)kTilePos;
-            if constexpr (FULL) {
-                // exactly kStores unconditional stores per thread
-                constexpr int kStores = kTilePos / 4 / TB;
-                static_assert(kStores * 4 * TB == kTilePos, "whole 16-B stores");
-                uint4 v[kStores];
+        // 4. the sorted tile goes out packed, three entries per u64, as 16-B
+        //    stores: thread t packs entries 6v .. 6v+5 for its vectors v.  In
+        //    a short tile the entries past its end are stale, masked so they
+        //    cannot spill into a neighbour field (pass 2 never uses them).
+        uint4 *dst = reinterpret_cast<uint4 *>(pos_out + tile * (size_t)kTileKeys);
+        constexpr int kVecs = kTileKeys / 2;  // 16-B vectors per tile
+        constexpr int kStores = kVecs / TB;
+        static_assert(kStores * TB == kVecs, "whole vectors per thread");
+        uint4 v[kStores];
 #pragma unroll
-                for (int r = 0; r < kStores; r++)
-                    v[r] = reinterpret_cast<const uint4 *>(s_sorted)[r * TB + tid];
+        for (int r = 0; r < kStores; r++) {
+            const uint2 *src = reinterpret_cast<const uint2 *>(s_sorted + 6 * (r * TB + tid));
+            const uint2 a = src[0], b = src[1], c = src[2];
+            uint32_t e[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+            if constexpr (!FULL) {
 #pragma unroll
-                for (int r = 0; r < kStores; r++)
-                    reinterpret_cast<uint4 *>(dst)[r * TB + tid] = v[r];
-            } else {
-                const int npos = tile_keys * 3;
-                const int nq = npos / 4;
-                for (int q = tid; q < nq; q += TB)
-                    reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(s_sorted)[q];
-                for (int e = nq * 4 + tid; e < npos; e += TB) dst[e] = s_sorted[e];
-                // the short last tile: pad with a position no segment holds,
-                // since pass 2 reads whole 16-B vectors and past run ends
-                for (int e = npos + tid; e < kTilePos; e += TB) dst[e] = 0xFFFFFFFFu;
+                for (int q = 0; q < 6; q++) e[q] &= kEntryMask;
             }
-        } else if constexpr (ABLATE == 1) {
-            if (s_sorted[tid] == 0xFFFFFFFFu) pos_out[tid] = 0;
+            v[r] = make_uint4(e[0] | (e[1] << 21), (e[1] >> 11) | (e[2] << 10),
+                              e[3] | (e[4] << 21), (e[4] >> 11) | (e[5] << 10));
         }
+#pragma unroll
+        for (int r = 0; r < kStores; r++) dst[r * TB + tid] = v[r];
     };
 
     // Full tiles in the loop; the short last tile (index ntiles - 1, always
     // in a block's final round) after it, so the loop sees only FULL.
     const size_t nfull = ks.n / kTileKeys;
-    if constexpr (STAGGER > 0) {  // timing builds (tools/ubench): delay the second half of the grid
-        if (blockIdx.x >= gridDim.x / 2)
-            for (int i = 0; i < STAGGER; i++) __builtin_amdgcn_s_sleep(127);
-    }
     size_t tile = part_tile(0, ntiles);
     if (tile < ntiles) load_tile_keys<LAYOUT, TB>(ks, tile, tid, kcur);
     size_t round = 0;
@@ -383,14 +380,7 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
 // go through the transpose: at C4 (805 MB) the column stores cost ~2.1 ms
 // (partial-line write-backs), the transpose 0.39 ms (tools/ubench.py part*).
 // ---------------------------------------------------------------------------
-// BLOOMHIP_COLUMN_TABLE_MAX (bytes) overrides the 16 MiB limit (tuning).
-static size_t column_table_max_bytes() {
-    static const size_t v = [] {
-        const char *e = getenv("BLOOMHIP_COLUMN_TABLE_MAX");
-        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(16u << 20);
-    }();
-    return v;
-}
+constexpr size_t kColumnTableMaxBytes = 16u << 20;  // larger run tables: rows + transpose
 constexpr int kTransposeTile = 64;
 constexpr int kTransposeBlock = 256;
 
@@ -419,59 +409,50 @@ __global__ void __launch_bounds__(kTransposeBlock) k_runs_transpose(
 // ---------------------------------------------------------------------------
 
 constexpr int kApplyBlock = 1024;
-constexpr int kApplyDepth = 2;  // lane-group loads per wave per batch (tools/ubench.py part*: 2 beat 1, 4, 8, 16 at C2/C4/C5)
+constexpr int kApplyDepth = 2;  // lane-group loads per wave per batch
 
-// Lanes per tile for pass 2, from the average run length L = kPartTilePos /
-// nbins.  A step of 4G entries per tile; runs longer than a step finish in
-// the wave-uniform tail loop.  Measured on MI355X (tools/ubench.py part*):
-// G = 8 beats G = 16 even at L = 48 (C2), G = 4 ~ G = 8 at L = 4 (C4), G = 2
-// is always worse (its loads cover too few bytes per lane group).
+// Lanes per tile for pass 2, from the average run length L = tile entries /
+// nbins: a step reads 6G entries of a tile (G lanes x one 16-B vector);
+// runs longer than a step finish in the wave-uniform tail loop.
 inline int apply_lanes_per_tile(size_t nbins, size_t tile_pos = kPartTilePos) {
     const size_t L = tile_pos / (nbins ? nbins : 1);
-    if (L < 10) return 4;
-    if (L < 96) return 8;
-    if (L < 192) return 16;
+    if (L < 16) return 4;
+    if (L < 144) return 8;
+    if (L < 288) return 16;
     return 32;
 }
 
 // MODE kApplyBuild: OR every entry into the zeroed LDS image, write the
 // segment.  kApplyProbe: the LDS image is the filter's segment; each entry's
 // bit is written as one result byte at the entry's own index in the sorted
-// tile (res[tile*kPartTilePos + index]), so the result stores follow the runs
-// like the loads.  kApplyStack: LDS holds bits [b*w, (b+1)*w) mod m_j of every stack
-// member j (StackTable), the result byte carries member j's bit at bit j.
-// (Writing the results over the positions instead, 4 B each, made the whole
-// probe slower: the combine then reads 4x the bytes; tools/ubench.py stack.)
+// tile (res[tile*kTilePos + index]), so the result stores follow the runs
+// like the loads.  kApplyStack: LDS holds bits [b*w, (b+1)*w) mod m_j of
+// every stack member j (StackTable), the result byte carries member j's bit
+// at bit j.
 //
 // The walk: G consecutive lanes share one tile and read its run as 16-B
-// vectors, lane j of the group starting at the run's 16-B-aligned start
-// + 4j, so one load instruction covers 64/G tiles x 4G entries.  The lanes
-// never test run bounds per entry: the sorted tile holds segment b's run
-// between runs of segments < b and > b, so an entry belongs to this segment
-// exactly when (position - base) < lim.  Reading past either end of the run
-// therefore only loads other segments' entries (the last tile's tail is
-// padded with 0xFFFFFFFF by pass 1), and lanes of tiles past the end re-read
-// the last tile, which ORs / writes the same values twice.  A wave owns
-// batches of kApplyDepth load groups; the next batch's run bounds are loaded
-// while the current one is applied, and the rare tile whose run outlasts the
-// first step is finished by a wave-uniform loop.
-// ABLATE (timing builds only): 1 = skip the LDS ORs (build), 2 = skip the
-// result stores (probe), 3 = non-temporal position loads, 4 = stage the LDS
-// image and stop.  The product launches 0.
+// vectors (two packed u64 = six entries), lane j of the group taking the
+// vector that holds the run's first entry + j, so one load instruction
+// covers 64/G tiles x 6G entries.  An entry is this segment's exactly when
+// its index lies in [run start, run end) (the bounds are already in the
+// lane's registers); its offset is (entry - b*S) mod 2^21.  Lanes of tiles
+// past the end re-read the last tile, which ORs / writes the same values
+// twice.  A wave owns batches of kApplyDepth load groups; the next batch's
+// run bounds are loaded while the current one is applied, and the rare tile
+// whose run outlasts the first step is finished by a wave-uniform loop.
 constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2;
 
-template <int MODE, int G, int ABLATE = 0, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth,
-          int TILE_POS = kPartTilePos>
+template <int MODE, int G, int TILE_KEYS, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth>
 __global__ void __launch_bounds__(BLOCK) k_part_apply(
-    const uint32_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
+    const uint64_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, uint32_t seg_bits, uint64_t m, uint32_t *__restrict__ words, uint64_t nw32,
     int merge_existing, uint8_t *__restrict__ res, StackTable st) {
     constexpr bool PROBE = MODE != kApplyBuild;
     static_assert(G >= 1 && G <= 64 && (64 % G) == 0, "G lanes per tile");
-    constexpr int kTPI = 64 / G;                     // tiles per load instruction
-    constexpr int kBatchTiles = kTPI * DEPTH;  // tiles per wave batch
-    constexpr uint32_t kStep = 4 * G;                // entries a tile advances per step
-    constexpr uint32_t kLastVec = TILE_POS - 4;
+    constexpr int kTilePos = 3 * TILE_KEYS;
+    constexpr int kTPI = 64 / G;                 // tiles per load instruction
+    constexpr int kBatchTiles = kTPI * DEPTH;   // tiles per wave batch
+    constexpr uint32_t kLastVec = TILE_KEYS / 2 - 1;
 
     const uint32_t seg_words = seg_bits / 32;
     extern __shared__ __attribute__((aligned(16))) uint32_t seg[];
@@ -482,8 +463,8 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const int b = (int)xcd_remap(blockIdx.x, (unsigned)nbins);
     const uint64_t w0 = (uint64_t)b * seg_words;
     const int nseg = (int)(min(nw32, w0 + seg_words) - w0);  // last segment may be short
-    const uint32_t base = (uint32_t)b * seg_bits;             // entries are full positions
-    const uint32_t lim = (uint32_t)min((uint64_t)seg_bits, m - base);
+    const uint64_t base = (uint64_t)b * seg_bits;
+    const uint32_t base21 = (uint32_t)base & kEntryMask;
     if constexpr (MODE == kApplyStack) {
         // member j's bits (b*w + o) mod m_j for o < w: the w bits from
         // (b*w) mod m_j on, wrapping at m_j (w <= m_j; w and m_j are
@@ -515,12 +496,11 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             reinterpret_cast<uint4 *>(seg)[i] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
-    if constexpr (ABLATE == 4) return;  // timing builds: staging only
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const uint32_t sub4 = (uint32_t)(lane % G) * 4;  // this lane's offset in its tile's step
-    const int tl = lane / G;                         // this lane's tile in a load group
+    const uint32_t sub = (uint32_t)(lane % G);  // this lane's vector in its tile's step
+    const int tl = lane / G;                    // this lane's tile in a load group
     const int nbatch = (ntiles + kBatchTiles - 1) / kBatchTiles;
 
     auto bounds = [&](int j, uint2 (&r)[DEPTH]) {
@@ -535,91 +515,57 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             }
         }
     };
-    auto load = [&](int t, uint32_t e) -> uint4 {
-        if constexpr (ABLATE == 3) {
-            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-            const v4u x = __builtin_nontemporal_load(
-                reinterpret_cast<const v4u *>(pos + (size_t)t * TILE_POS + e));
-            return make_uint4(x[0], x[1], x[2], x[3]);
-        }
-        return *reinterpret_cast<const uint4 *>(pos + (size_t)t * TILE_POS + e);
+    auto load = [&](int t, uint32_t vi) -> uint4 {
+        return reinterpret_cast<const uint4 *>(pos + (size_t)t * TILE_KEYS)[vi];
     };
-    auto apply1 = [&](uint32_t v, int t, uint32_t e) {
-        const uint32_t o = v - base;
-        if constexpr (ABLATE == 1) {
-            asm volatile("" ::"v"(o));
-            (void)t; (void)e;
-        } else if (o < lim) {
-            if constexpr (PROBE) {  // (ABLATE builds only; apply4 handles probes)
-                res[(size_t)t * TILE_POS + e] = (seg[o >> 5] >> (o & 31)) & 1u;
-            } else {
-                (void)t; (void)e;
-                atomicOr(&seg[o >> 5], 1u << (o & 31));
-            }
-        }
-    };
-    auto apply4 = [&](const uint4 &v, int t, uint32_t e) {
-        if constexpr (PROBE && ABLATE != 1) {
-            // the 4 result bytes go out as one dword when all 4 entries are
-            // this segment's (inside a run), else byte by byte
-            // LDS reads unconditional (offset 0 for other segments' entries),
-            // so they issue back to back under one wait
-            const uint32_t o[4] = {v.x - base, v.y - base, v.z - base, v.w - base};
-            uint32_t bits = 0, mask = 0;
-            if constexpr (MODE == kApplyStack) {
-                uint32_t r[4] = {0u, 0u, 0u, 0u};
+    // The six entries of vector vi of tile t; run = [r.x, r.y).
+    auto apply6 = [&](const uint4 &v, int t, uint32_t vi, const uint2 &r) {
+        const uint32_t e[6] = {v.x & kEntryMask, __builtin_amdgcn_alignbit(v.y, v.x, 21) & kEntryMask,
+                               v.y >> 10,        v.z & kEntryMask,
+                               __builtin_amdgcn_alignbit(v.w, v.z, 21) & kEntryMask, v.w >> 10};
+        const uint32_t i0 = 6 * vi - r.x, len = r.y - r.x;  // entry k is in the run iff i0 + k < len
+        if constexpr (!PROBE) {
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t ok = o[k] < lim ? 1u : 0u;
-                    mask |= ok << k;
-                    const uint32_t oo = ok ? o[k] : 0u;
-                    const uint32_t *wp = seg + __umul24(oo >> 5, (uint32_t)st.nf);
-                    const uint32_t sh = oo & 31;
-#pragma unroll
-                    for (int j = 0; j < kMaxStack; j++)  // member j's word at immediate offset 4j
-                        if (j < st.nf) r[k] |= __builtin_amdgcn_ubfe(wp[j], sh, 1u) << j;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++) bits |= (mask >> k & 1u) ? r[k] << (8 * k) : 0u;
-            } else {
-                uint32_t w[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) w[k] = seg[o[k] < lim ? o[k] >> 5 : 0u];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t ok = o[k] < lim ? 1u : 0u;
-                    mask |= ok << k;
-                    bits |= (((w[k] >> (o[k] & 31)) & ok) << (8 * k));
-                }
-            }
-            uint8_t *p = res + (size_t)t * TILE_POS + e;
-            if constexpr (ABLATE == 2) {
-                asm volatile("" ::"v"(bits), "v"(mask));
-                (void)p;
-            } else if (mask == 0xFu) {
-                *reinterpret_cast<uint32_t *>(p) = bits;
-            } else if (mask != 0) {
-                // a run edge: each aligned half that is wholly this segment's
-                // goes out as one 2-byte store, the rest byte by byte
-                // (p is 4-byte aligned: e is a multiple of 4)
-                if ((mask & 3u) == 3u) {
-                    *reinterpret_cast<uint16_t *>(p) = (uint16_t)bits;
-                } else {
-                    if (mask & 1u) p[0] = (uint8_t)bits;
-                    if (mask & 2u) p[1] = (uint8_t)(bits >> 8);
-                }
-                if ((mask & 12u) == 12u) {
-                    *reinterpret_cast<uint16_t *>(p + 2) = (uint16_t)(bits >> 16);
-                } else {
-                    if (mask & 4u) p[2] = (uint8_t)(bits >> 16);
-                    if (mask & 8u) p[3] = (uint8_t)(bits >> 24);
+            for (int k = 0; k < 6; k++) {
+                if (i0 + k < len) {
+                    const uint32_t o = (e[k] - base21) & kEntryMask;
+                    atomicOr(&seg[o >> 5], 1u << (o & 31));
                 }
             }
         } else {
-            apply1(v.x, t, e);
-            apply1(v.y, t, e + 1);
-            apply1(v.z, t, e + 2);
-            apply1(v.w, t, e + 3);
+            uint32_t bits[6], mask = 0;
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                const uint32_t ok = i0 + k < len ? 1u : 0u;
+                mask |= ok << k;
+                const uint32_t o = ok ? (e[k] - base21) & kEntryMask : 0u;  // reads stay in the image
+                if constexpr (MODE == kApplyStack) {
+                    const uint32_t *wp = seg + __umul24(o >> 5, (uint32_t)st.nf);
+                    const uint32_t sh = o & 31;
+                    uint32_t acc = 0;
+#pragma unroll
+                    for (int j = 0; j < kMaxStack; j++)  // member j's word at immediate offset 4j
+                        if (j < st.nf) acc |= __builtin_amdgcn_ubfe(wp[j], sh, 1u) << j;
+                    bits[k] = acc;
+                } else {
+                    bits[k] = (seg[o >> 5] >> (o & 31)) & 1u;
+                }
+            }
+            // six result bytes at 6*vi (2-byte aligned): whole pairs as
+            // 2-byte stores, a run's edge byte by byte
+            uint8_t *p = res + (size_t)t * kTilePos + 6 * vi;
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const uint32_t mq = (mask >> (2 * q)) & 3u;
+                if (mq == 3u) {
+                    *reinterpret_cast<uint16_t *>(p + 2 * q) =
+                        (uint16_t)(bits[2 * q] | (bits[2 * q + 1] << 8));
+                } else if (mq == 1u) {
+                    p[2 * q] = (uint8_t)bits[2 * q];
+                } else if (mq == 2u) {
+                    p[2 * q + 1] = (uint8_t)bits[2 * q + 1];
+                }
+            }
         }
     };
 
@@ -627,24 +573,24 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     if (wave < nbatch) bounds(wave, r);
     for (int j = wave; j < nbatch; j += (BLOCK / 64)) {
         int t[DEPTH];
-        uint32_t e[DEPTH];
+        uint32_t vi[DEPTH];
         uint4 v[DEPTH];
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) {
             t[d] = min(j * kBatchTiles + d * kTPI + tl, ntiles - 1);
-            e[d] = (r[d].x & ~3u) + sub4;
-            v[d] = load(t[d], min(e[d], kLastVec));
+            vi[d] = min(r[d].x / 6u + sub, kLastVec);
+            v[d] = load(t[d], vi[d]);
         }
         uint2 rn[DEPTH];
         const int jn = j + (BLOCK / 64);
         if (jn < nbatch) bounds(jn, rn);
 #pragma unroll
-        for (int d = 0; d < DEPTH; d++) apply4(v[d], t[d], min(e[d], kLastVec));
+        for (int d = 0; d < DEPTH; d++) apply6(v[d], t[d], vi[d], r[d]);
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) {
-            for (uint32_t en = e[d] + kStep; __ballot(en < r[d].y) != 0; en += kStep) {
-                const uint32_t ec = min(en, kLastVec);
-                apply4(load(t[d], ec), t[d], ec);
+            for (uint32_t vn = r[d].x / 6u + sub + G; __ballot(6 * vn < r[d].y) != 0; vn += G) {
+                const uint32_t vc = min(vn, kLastVec);
+                apply6(load(t[d], vc), t[d], vc, r[d]);
             }
         }
 #pragma unroll
@@ -1155,35 +1101,51 @@ int device_cu_count() {
     return cus[dev];
 }
 
+// The exact multiply-high divisor of SegMap: ceil(2^32 / g), accepted only
+// when mulhi(q, magic) == q / g for every q < nsub (checked here, once per
+// plan: nsub <= kPartMaxSub).
+static bool seg_magic(uint32_t g, uint32_t nsub, uint32_t *magic) {
+    if (g <= 1) {
+        *magic = 0;
+        return true;
+    }
+    const uint32_t M = (uint32_t)(((1ull << 32) + g - 1) / g);
+    for (uint32_t q = 0; q < nsub; q++)
+        if ((uint32_t)(((uint64_t)q * M) >> 32) != q / g) return false;
+    *magic = M;
+    return true;
+}
+
 bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
-    if (m == 0 || m > 0xFFFFFFFFull || ncu <= 0) return false;
+    if (m == 0 || ncu <= 0) return false;
     // Pass-2 segments: a multiple W of the CU count, each fitting in LDS.
     // Segment images up to all 160 KiB of a CU's LDS (pass 2 has no static
-    // LDS): C5 gets 512 segments instead of 768, runs 1.5x longer, pass 2
-    // 0.302 -> 0.263 ms.  BLOOMHIP_SEG_MAX_KIB (16..160) overrides (tuning).
-    static const uint64_t seg_max = [] {
-        const char *e = getenv("BLOOMHIP_SEG_MAX_KIB");
-        const uint64_t k = e ? strtoull(e, nullptr, 10) : 0;
-        return (k >= 16 && k <= 160) ? k * 1024 * 8 : (uint64_t)kStackMaxBits;
-    }();
+    // LDS): C5 gets 512 segments instead of 768, runs 1.5x longer.
+    const uint64_t seg_max = kStackMaxBits;
     const uint64_t per_round = (uint64_t)ncu * seg_max;
     const uint64_t W = ((m + per_round - 1) / per_round) * (uint64_t)ncu;
-    // Sub-segments: the smallest power of two 2^s with at most kPartMaxBins
-    // of them, then g = ceil(nsub / W) per segment, while g << s fits LDS.
+    // q = p >> s: the smallest power of two 2^s with at most kPartMaxSub
+    // values, then g = ceil(nsub / W) per segment, while g << s fits LDS.
     uint32_t s = 5;  // >= one 32-bit word
-    while ((((m - 1) >> s) + 1) > kPartMaxBins) s++;
+    while ((((m - 1) >> s) + 1) > kPartMaxSub) s++;
     uint64_t nsub = ((m - 1) >> s) + 1;
     uint64_t g = (nsub + W - 1) / W;
     while (g > 1 && (g << s) > seg_max) g--;
-    if ((g << s) > seg_max) return false;
+    if ((g << s) > seg_max) return false;  // m > kPartMaxSub * 2^20
     // 128-B aligned segments for the 16-B segment stores.
     while (((g << s) % 1024) != 0) g++;
     if ((g << s) > seg_max) return false;
+    const uint64_t nbins = (nsub + g - 1) / g;
+    if (nbins > kPartMaxBinsBig || (nbins > kPartMaxBins && choose_tile_keys(nbins) == kPartTileKeys))
+        return false;
+    uint32_t magic = 0;
+    if (!seg_magic((uint32_t)g, (uint32_t)nsub, &magic)) return false;
     ws->sub_shift = s;
     ws->group = (uint32_t)g;
     ws->nsub = (uint32_t)nsub;
     ws->seg_bits = (uint32_t)(g << s);
-    ws->nbins = (size_t)((nsub + g - 1) / g);
+    ws->nbins = (size_t)nbins;
+    ws->magic = magic;
     return true;
 }
 
@@ -1194,23 +1156,14 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
         return false;
     // Segment widths w: w | gcd_m, so every member is a whole number of
     // segments, in at most 144 KiB of images (two pass-2 workgroups per CU
-    // when they fit in 80 KiB).  BLOOMHIP_STACK_WRAP=1 (tuning experiments)
-    // asks only w | m_max and w <= m_min, in up to 160 KiB: the staging reads
-    // each member from (b*w) mod m_j with wraparound.  At C3 that doubles w
-    // (640 segments instead of 1280, one workgroup per CU) and was no faster:
-    // pass 1 121 vs 129 us, pass 2 163 vs 153 us (profiles/r01/s3/).
-    static const bool wrap = [] {
-        const char *e = getenv("BLOOMHIP_STACK_WRAP");
-        return e && e[0] == '1';
-    }();
-    const uint64_t divisor = wrap ? m_max : gcd_m;
-    const uint64_t wmax = (wrap ? kStackMaxBits : kSegMaxBits) / (uint64_t)nf;
+    // when they fit in 80 KiB).
+    const uint64_t wmax = kSegMaxBits / (uint64_t)nf;
     uint32_t s0 = 5;
     while ((((m_max - 1) >> s0) + 1) > kPartMaxBins) s0++;
     // candidates w = g << s, 128-bit multiples for the 16-B image loads
     uint64_t best_w = 0;
     uint32_t best_s = 0;
-    // The segment count sets the run length per tile (kPartTilePos / nbins),
+    // The segment count sets the run length per tile (tile entries / nbins),
     // w only the LDS image: the widest w that still gives every CU a segment,
     // else (small m_max) the narrowest, for the most segments.
     auto better = [&](uint64_t w) {
@@ -1220,10 +1173,10 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
         return a ? w > best_w : w < best_w;
     };
     for (uint32_t s = s0; s < 32 && (1ull << s) <= wmax; s++) {
-        if (divisor % (1ull << s)) break;  // larger s cannot divide either
+        if (gcd_m % (1ull << s)) break;  // larger s cannot divide either
         for (uint64_t g = wmax >> s; g >= 1; g--) {
             const uint64_t w = g << s;
-            if (w % 128 || divisor % w || w > m_min) continue;
+            if (w % 128 || gcd_m % w || w > m_min || m_max / w > kPartMaxBinsBig) continue;
             if (better(w) || (w == best_w && s > best_s)) {
                 best_w = w;
                 best_s = s;
@@ -1231,11 +1184,15 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
         }
     }
     if (best_w == 0) return false;
+    const uint32_t g = (uint32_t)(best_w >> best_s), nsub = (uint32_t)(m_max >> best_s);
+    uint32_t magic = 0;
+    if (!seg_magic(g, nsub, &magic)) return false;
     ws->sub_shift = best_s;
-    ws->group = (uint32_t)(best_w >> best_s);
-    ws->nsub = (uint32_t)(m_max >> best_s);
+    ws->group = g;
+    ws->nsub = nsub;
     ws->seg_bits = (uint32_t)best_w;
     ws->nbins = (size_t)(m_max / best_w);
+    ws->magic = magic;
     return true;
 }
 
@@ -1250,26 +1207,34 @@ hipError_t launch_runs_transpose(const PartitionWorkspace &ws, hipStream_t strea
 }
 
 bool runs_as_columns(const PartitionWorkspace &ws) {
-    return ws.ntiles * (ws.nbins + 1) * 4 <= column_table_max_bytes();
+    return ws.ntiles * (ws.nbins + 1) * 4 <= kColumnTableMaxBytes;
 }
 
 template <bool SLOTS, int TB>
 hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                          uint16_t *slots, hipStream_t stream) {
+    if (ws.nbins > (TB >= 1024 ? kPartMaxBinsBig : kPartMaxBins)) return hipErrorInvalidValue;
     const unsigned grid = part_bin_grid(ws.ntiles, TB);
     const bool cols = runs_as_columns(ws);
     uint32_t *runs = cols ? ws.run_starts : ws.run_rows;
-    const int nb = (int)ws.nbins, ns = (int)ws.nsub, sh = (int)ws.sub_shift, g = (int)ws.group;
-#define BIN_LAUNCH(L, C)                                                                     \
-    do {                                                                                     \
-        k_part_bin<L, 0, SLOTS, C, TB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, nb,    \
-                                                                  ns, sh, g, ws.ntiles, slots); \
+    const SegMap sm = seg_map_of(ws);
+    const bool wide = !mp.fast;
+#define BIN_LAUNCH(L, C, W)                                                                   \
+    k_part_bin<L, SLOTS, C, TB, W><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm, ws.ntiles, \
+                                                            slots)
+#define BIN_LAYOUT(L)                                         \
+    do {                                                      \
+        if (wide) {                                           \
+            if (cols) BIN_LAUNCH(L, true, true);              \
+            else BIN_LAUNCH(L, false, true);                  \
+        } else {                                              \
+            if (cols) BIN_LAUNCH(L, true, false);             \
+            else BIN_LAUNCH(L, false, false);                 \
+        }                                                     \
     } while (0)
-    if (ks.layout == KEYS_PACKED) {
-        if (cols) BIN_LAUNCH(KEYS_PACKED, true); else BIN_LAUNCH(KEYS_PACKED, false);
-    } else {
-        if (cols) BIN_LAUNCH(KEYS_STRIDED, true); else BIN_LAUNCH(KEYS_STRIDED, false);
-    }
+    if (ks.layout == KEYS_PACKED) BIN_LAYOUT(KEYS_PACKED);
+    else BIN_LAYOUT(KEYS_STRIDED);
+#undef BIN_LAYOUT
 #undef BIN_LAUNCH
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess || cols) return e;
@@ -1294,13 +1259,12 @@ hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const Partiti
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
-template <int MODE, int G, int TP>
+template <int MODE, int G, int TK>
 hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                           uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                           hipStream_t stream) {
     static const bool attr_set = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(
-                                      &k_part_apply<MODE, G, 0, kApplyBlock, kApplyDepth, TP>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<MODE, G, TK>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kStackMaxBits / 8));
         return true;
@@ -1308,28 +1272,21 @@ hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *wo
     (void)attr_set;
     const size_t lds = (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
     if (lds > kStackMaxBits / 8) return hipErrorInvalidValue;
-    k_part_apply<MODE, G, 0, kApplyBlock, kApplyDepth, TP><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
+    k_part_apply<MODE, G, TK><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
         res, st);
     return hipGetLastError();
 }
 
-template <int MODE, int TP>
-hipError_t launch_apply_tp(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
+template <int MODE, int TK>
+hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                            uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                            hipStream_t stream) {
-    // BLOOMHIP_APPLY_LANES forces G (tuning experiments)
-    static const int g_env = [] {
-        const char *e = getenv("BLOOMHIP_APPLY_LANES");
-        return e ? atoi(e) : 0;
-    }();
-    switch (g_env ? g_env : apply_lanes_per_tile(ws.nbins, TP)) {
-        case 2: return launch_apply_g<MODE, 2, TP>(ws, m, words, nw32, merge, res, st, stream);
-        case 4: return launch_apply_g<MODE, 4, TP>(ws, m, words, nw32, merge, res, st, stream);
-        case 8: return launch_apply_g<MODE, 8, TP>(ws, m, words, nw32, merge, res, st, stream);
-        case 16: return launch_apply_g<MODE, 16, TP>(ws, m, words, nw32, merge, res, st, stream);
-        case 32: return launch_apply_g<MODE, 32, TP>(ws, m, words, nw32, merge, res, st, stream);
-        default: return launch_apply_g<MODE, 64, TP>(ws, m, words, nw32, merge, res, st, stream);
+    switch (apply_lanes_per_tile(ws.nbins, 3 * TK)) {
+        case 4: return launch_apply_g<MODE, 4, TK>(ws, m, words, nw32, merge, res, st, stream);
+        case 8: return launch_apply_g<MODE, 8, TK>(ws, m, words, nw32, merge, res, st, stream);
+        case 16: return launch_apply_g<MODE, 16, TK>(ws, m, words, nw32, merge, res, st, stream);
+        default: return launch_apply_g<MODE, 32, TK>(ws, m, words, nw32, merge, res, st, stream);
     }
 }
 
@@ -1337,35 +1294,23 @@ template <int MODE>
 hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *words, uint64_t nw32,
                         int merge, uint8_t *res, const StackTable &st, hipStream_t stream) {
     return tile_keys_of(ws) == 2 * kPartTileKeys
-               ? launch_apply_tp<MODE, 2 * kPartTilePos>(ws, m, words, nw32, merge, res, st, stream)
-               : launch_apply_tp<MODE, kPartTilePos>(ws, m, words, nw32, merge, res, st, stream);
+               ? launch_apply_tk<MODE, 2 * (int)kPartTileKeys>(ws, m, words, nw32, merge, res, st,
+                                                               stream)
+               : launch_apply_tk<MODE, (int)kPartTileKeys>(ws, m, words, nw32, merge, res, st,
+                                                           stream);
 }
 
-// The combine for the batch's tile size.
+// The combine for the batch's tile size (1024 threads: 42 us at C3 against
+// 45 for 512 and 53 for 256).
 hipError_t launch_combine(const PartitionWorkspace &ws, const uint8_t *res, const uint16_t *slots,
                           size_t n, uint64_t *out, size_t nw, const StackTable &rows,
                           hipStream_t stream) {
-    // workgroup size: BLOOMHIP_COMBINE_BLOCK (256 / 512 / 1024) for tuning
-    static const int cb = [] {
-        const char *e = getenv("BLOOMHIP_COMBINE_BLOCK");
-        const int v = e ? atoi(e) : kCombineBlockDefault;
-        return (v == 256 || v == 512 || v == 1024) ? v : kCombineBlockDefault;
-    }();
-#define COMBINE(TK, CB) \
-    k_probe_combine<TK, CB><<<(unsigned)ws.ntiles, CB, 0, stream>>>(res, slots, n, out, nw, rows)
-#define COMBINE_CB(TK)                           \
-    switch (cb) {                                \
-        case 256: COMBINE(TK, 256); break;       \
-        case 512: COMBINE(TK, 512); break;       \
-        default: COMBINE(TK, 1024); break;       \
-    }
-    if (tile_keys_of(ws) == 2 * kPartTileKeys) {
-        COMBINE_CB(2 * (int)kPartTileKeys)
-    } else {
-        COMBINE_CB((int)kPartTileKeys)
-    }
-#undef COMBINE_CB
-#undef COMBINE
+    if (tile_keys_of(ws) == 2 * kPartTileKeys)
+        k_probe_combine<2 * (int)kPartTileKeys, kCombineBlockDefault>
+            <<<(unsigned)ws.ntiles, kCombineBlockDefault, 0, stream>>>(res, slots, n, out, nw, rows);
+    else
+        k_probe_combine<(int)kPartTileKeys, kCombineBlockDefault>
+            <<<(unsigned)ws.ntiles, kCombineBlockDefault, 0, stream>>>(res, slots, n, out, nw, rows);
     return hipGetLastError();
 }
 
@@ -1463,7 +1408,6 @@ hipError_t launch_route(const KeySpan &ks, const RouteTable &t, uint64_t *cand, 
     const size_t per_block = (in_lds ? lds : 0) + 2048;
     int per_cu = (int)(kLdsBitmapBytes / per_block);
     per_cu = per_cu < 1 ? 1 : per_cu > 8 ? 8 : per_cu;  // 8 x 256 threads = 32 waves per CU
-    if (const char *e = getenv("BLOOMHIP_ROUTE_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
     const unsigned grid = grid_for(nw, kRouteBlock / 64, (unsigned)(device_cu_count() * per_cu));
 #define ROUTE_LAUNCH(L, F, R) \
     k_route<L, F, R><<<grid, kRouteBlock, F ? lds : 0, stream>>>(ks, t, cand, nw, first, page)

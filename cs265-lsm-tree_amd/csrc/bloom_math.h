@@ -14,7 +14,9 @@
 //      precomputed reciprocal v = floor((2^64-1)/d) - 2^32 (Möller & Granlund,
 //      "Improved division by invariant integers", IEEE TC 2011, Alg. 4),
 //      keeping only the remainder.
-// Larger m falls back to the compiler's 64-bit remainder (exact, slower).
+// For 2^32 <= m <= 2^46 (bloomhip_create's bound) mod_wide estimates the
+// quotient in double precision and corrects it with one exact 64-bit
+// multiply-subtract (see there); no integer division either.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -87,6 +89,7 @@ struct ModParams {
     uint32_t l;   // leading zeros of m as a u32     (fast path)
     uint32_t fast;  // 1 when m <= 0xFFFFFFFF
     uint32_t pad;
+    double minv;  // 1.0 / m                         (wide path)
 };
 
 // Host-side precomputation (m >= 1).
@@ -103,6 +106,7 @@ inline ModParams make_mod_params(uint64_t m) {
         p.v = (uint32_t)(~0ull / dn - (1ull << 32));
         p.R = (uint32_t)((1ull << 32) % m);
     }
+    p.minv = m ? 1.0 / (double)m : 0.0;
     return p;
 }
 
@@ -121,8 +125,23 @@ BH_HD uint32_t mod_fast(uint64_t x, const ModParams &p) {
     return r >> p.l;
 }
 
+// x % m for 2^32 <= m <= 2^46.  q = trunc(double(x) * (1/m)): x < 2^64 and
+// m >= 2^32 make x/m < 2^32, and the three roundings (x to double, 1/m, the
+// product) err by under 2^-50 relative, i.e. under 2^-18 absolute, so q is
+// floor(x/m) or one off either way.  r = x - q*m in wrapping 64-bit
+// arithmetic is then r_true - m (negative as int64: r < m < 2^46), r_true, or
+// r_true + m (in [m, 2m)), fixed by one conditional add or subtract.
+// tests/test_host.py fuzzes it against the oracle's exact remainder.
+BH_HD uint64_t mod_wide(uint64_t x, const ModParams &p) {
+    const uint64_t q = (uint64_t)((double)x * p.minv);
+    uint64_t r = x - q * p.m;
+    if ((int64_t)r < 0) r += p.m;
+    else if (r >= p.m) r -= p.m;
+    return r;
+}
+
 BH_HD uint64_t mod_any(uint64_t x, const ModParams &p) {
-    return p.fast ? (uint64_t)mod_fast(x, p) : x % p.m;
+    return p.fast ? (uint64_t)mod_fast(x, p) : mod_wide(x, p);
 }
 
 // ---- exact q = x / S for 32-bit x, runtime S >= 2 (Granlund–Montgomery,

@@ -150,106 +150,61 @@ extern "C" int ubench_run(int which, void *dbuf, size_t bytes, uint64_t m, int g
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-// Pass 1 of the partition build: 0 = the product's launch, 1..3 = pass 1
-// with phases removed (ABLATE), 4 = pass 1 writing run-start columns, 5 =
-// pass 1 writing rows, 6 = the row -> column transpose alone.
-extern "C" int ubench_part_bin(int ablate, const void *keys, size_t n, uint64_t m, uint32_t *pos,
-                               uint32_t *run_starts, void *stream) {
+// Geometry of the product's partition build of n keys into m bits
+// (tools/ubench.py sizes its buffers from it): segments, segment bits, tile
+// keys and tiles.
+extern "C" int ubench_part_geometry(size_t n, uint64_t m, uint64_t *out4) {
+    PartitionWorkspace ws{};
+    if (!plan_segments(m, device_cu_count(), &ws)) return -34;
+    const size_t tk = choose_tile_keys(ws.nbins);
+    out4[0] = ws.nbins;
+    out4[1] = ws.seg_bits;
+    out4[2] = tk;
+    out4[3] = (n + tk - 1) / tk;
+    return 0;
+}
+
+// Phases of the product's partition build (tools/ubench.py part): variant 0 =
+// pass 1 (launch_part_bin: the product's tile, table layout and transpose),
+// 1 = pass 2 as the product launches it, G in {4, 8, 16, 32} = pass 2 with G
+// lanes per tile.  pos: ntiles * tile_keys u64; runs: both table layouts.
+extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, uint64_t *pos,
+                           uint32_t *runs, uint32_t *words, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
     const ModParams mp = make_mod_params(m);
     PartitionWorkspace ws{};
     if (!plan_segments(m, device_cu_count(), &ws)) return -34;
-    const int nbins = (int)ws.nbins;
-    const size_t ntiles = (n + kPartTileKeys - 1) / kPartTileKeys;
-    const unsigned grid = part_bin_grid(ntiles);
-    const int nsub = (int)ws.nsub, ssh = (int)ws.sub_shift, grp = (int)ws.group;
-    // run_starts holds both layouts: segment-major first, the pass-1 rows after
-    ws.ntiles = ntiles;
-    ws.run_starts = run_starts;
-    ws.run_rows = run_starts + ntiles * (ws.nbins + 1);
-    uint32_t *rows = ws.run_rows;
-    switch (ablate) {
-        case 0:
-            ws.pos = pos;
-            if (launch_part_bin(ks, mp, ws, s) != hipSuccess) return -5;
-            break;
-        case 1: k_part_bin<KEYS_PACKED, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, rows, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 2: k_part_bin<KEYS_PACKED, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, rows, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 3: k_part_bin<KEYS_PACKED, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, rows, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 4: k_part_bin<KEYS_PACKED, 0, false, true><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 5: k_part_bin<KEYS_PACKED, 0, false, false><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, rows, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 6: if (launch_runs_transpose(ws, s) != hipSuccess) return -5; break;
-        case 7:  // pass 1 (columns) with one workgroup per CU, leaving LDS for a concurrent pass 2
-            k_part_bin<KEYS_PACKED, 0, false, true><<<(unsigned)device_cu_count(), kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr);
-            break;
-        // 8..10: the product's pass 1 with the second half of the grid
-        // started 1..3 x 8K cycles late (do the two workgroups of a CU run
-        // their VALU and LDS phases in step?)
-        case 8: k_part_bin<KEYS_PACKED, 0, false, true, kPartBlock, 1><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 9: k_part_bin<KEYS_PACKED, 0, false, true, kPartBlock, 2><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        case 10: k_part_bin<KEYS_PACKED, 0, false, true, kPartBlock, 3><<<grid, kPartBlock, 0, s>>>(ks, mp, pos, run_starts, nbins, nsub, ssh, grp, ntiles, nullptr); break;
-        default: return -22;
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -5;
-}
-
-// Pass 2 of the partition build on the positions of ubench_part_bin ablate 0:
-// variant G in {2..64} = the product walk with G lanes per tile, 100 + G =
-// the same with the LDS ORs skipped (loads only), 0 = the product's choice.
-extern "C" int ubench_part_apply(int variant, const uint32_t *pos, const uint32_t *run_starts,
-                                 size_t n, uint64_t m, uint32_t *words, void *stream) {
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    PartitionWorkspace ws{};
-    if (!plan_segments(m, device_cu_count(), &ws)) return -34;
-    const int nbins = (int)ws.nbins;
-    const int ntiles = (int)((n + kPartTileKeys - 1) / kPartTileKeys);
+    ws.tile_keys = choose_tile_keys(ws.nbins);
+    ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
+    ws.pos = pos;
+    ws.run_rows = runs;
+    ws.run_starts = runs + ws.ntiles * (ws.nbins + 1);
     const uint64_t nw32 = ((m + 63) / 64) * 2;
-    const uint32_t sb = ws.seg_bits;
-    if (variant == 0) variant = apply_lanes_per_tile(ws.nbins);
-#define UB_APPLY(G, A) UB_APPLYD(G, A, kApplyDepth)
-#define UB_APPLYD(G, A, D)                                                                    \
-    do {                                                                                      \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<kApplyBuild, G, A, kApplyBlock, D>), \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,                 \
-                                  (int)(kSegMaxBits / 8));                                    \
-        k_part_apply<kApplyBuild, G, A, kApplyBlock, D><<<nbins, kApplyBlock, sb / 8, s>>>(         \
-            pos, run_starts, ntiles, nbins, sb, m, words, nw32, 0, nullptr, StackTable{});    \
-    } while (0)
+    hipError_t e = hipSuccess;
+    const bool big = ws.tile_keys == 2 * kPartTileKeys;
     switch (variant) {
-        case 2: UB_APPLY(2, 0); break;
-        case 4: UB_APPLY(4, 0); break;
-        case 8: UB_APPLY(8, 0); break;
-        case 16: UB_APPLY(16, 0); break;
-        case 32: UB_APPLY(32, 0); break;
-        case 64: UB_APPLY(64, 0); break;
-        case 402: UB_APPLYD(2, 0, 2); break;   // 400 + G: depth 2, 500 + G: depth 1
-        case 404: UB_APPLYD(4, 0, 2); break;
-        case 408: UB_APPLYD(8, 0, 2); break;
-        case 416: UB_APPLYD(16, 0, 2); break;
-        case 502: UB_APPLYD(2, 0, 1); break;
-        case 504: UB_APPLYD(4, 0, 1); break;
-        case 508: UB_APPLYD(8, 0, 1); break;
-        case 516: UB_APPLYD(16, 0, 1); break;
-        case 102: UB_APPLY(2, 1); break;
-        case 104: UB_APPLY(4, 1); break;
-        case 108: UB_APPLY(8, 1); break;
-        case 116: UB_APPLY(16, 1); break;
-        case 132: UB_APPLY(32, 1); break;
+        case 0: e = launch_part_bin(ks, mp, ws, s); break;
+        case 1: e = launch_part_apply(mp, words, ws, 0, s); break;
+#define UB_G(G)                                                                                   \
+    case G:                                                                                       \
+        e = big ? launch_apply_g<kApplyBuild, G, 2 * (int)kPartTileKeys>(ws, m, words, nw32, 0,   \
+                                                                        nullptr, StackTable{}, s) \
+                : launch_apply_g<kApplyBuild, G, (int)kPartTileKeys>(ws, m, words, nw32, 0,       \
+                                                                    nullptr, StackTable{}, s);    \
+        break;
+        UB_G(4) UB_G(8) UB_G(16) UB_G(32)
+#undef UB_G
         default: return -22;
     }
-#undef UB_APPLY
-#undef UB_APPLYD
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return e == hipSuccess ? 0 : -5;
 }
 
 // The stacked probe (C3 by default) by phase: 0 = the product's three
-// launches, 1 = pass 1 (with slots), 2 = pass 2 alone (G from
-// apply_lanes_per_tile), 3 = pass 2 without its result stores, 4 = pass 2
-// reading only member 0's image, 5 = the combine; 100 + G = pass 2 with G
-// lanes per tile.  Buffers sized by the caller for plan_stack's geometry
-// (ubench_stack_geometry; runs: both layouts).  Members must divide the
-// largest, so their gcd is the smallest.
+// launches, 1 = pass 1 (with slots), 2 = pass 2, 5 = the combine; 100 + G =
+// pass 2 with G lanes per tile.  Buffers sized by the caller for plan_stack's
+// geometry (ubench_stack_geometry; runs: both layouts).  Members must divide
+// the largest, so their gcd is the smallest.
 namespace {
 bool ub_stack_plan(int nf, const uint64_t *ms, uint64_t *mmax, PartitionWorkspace *ws) {
     uint64_t g = 0;
@@ -273,7 +228,7 @@ extern "C" int ubench_stack_geometry(int nf, const uint64_t *ms, uint64_t *nbins
 }
 
 extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, const uint64_t *ms,
-                            void *const *words, uint32_t *pos, uint32_t *runs, uint8_t *res,
+                            void *const *words, uint64_t *pos, uint32_t *runs, uint8_t *res,
                             uint16_t *slots, uint64_t *out, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
@@ -294,75 +249,23 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
     }
     const ModParams mp = make_mod_params(mmax);
     const size_t nw = (n + 63) / 64;
-    const size_t lds = (size_t)ws.seg_bits / 8 * nf;
-#define UB_STACK(G, A, T) UB_STACKB(G, A, T, kApplyBlock)
-#define UB_STACKT(G, A, T, B, TP)                                                                  \
-    do {                                                                                           \
-        (void)hipFuncSetAttribute(                                                                 \
-            reinterpret_cast<const void *>(&k_part_apply<kApplyStack, G, A, B, kApplyDepth, TP>),  \
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kStackMaxBits / 8));                 \
-        k_part_apply<kApplyStack, G, A, B, kApplyDepth, TP><<<(unsigned)ws.nbins, B, lds, s>>>(    \
-            ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, mmax, nullptr, 0,   \
-            0, res, T);                                                                            \
-    } while (0)
-#define UB_STACKD(G, D)                                                                            \
-    do {                                                                                           \
-        if (ws.tile_keys == 2 * kPartTileKeys) {                                                   \
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(                              \
-                &k_part_apply<kApplyStack, G, 0, kApplyBlock, D, 2 * kPartTilePos>),               \
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kStackMaxBits / 8));             \
-            k_part_apply<kApplyStack, G, 0, kApplyBlock, D, 2 * kPartTilePos>                      \
-                <<<(unsigned)ws.nbins, kApplyBlock, lds, s>>>(ws.pos, ws.run_starts,               \
-                (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, mmax, nullptr, 0, 0, res, st);         \
-        } else {                                                                                   \
-            return -22;                                                                            \
-        }                                                                                          \
-    } while (0)
-#define UB_STACKB(G, A, T, B)                                                                      \
-    do {                                                                                           \
-        if (ws.tile_keys == 2 * kPartTileKeys) UB_STACKT(G, A, T, B, 2 * kPartTilePos);            \
-        else UB_STACKT(G, A, T, B, kPartTilePos);                                                  \
-    } while (0)
-    const int G = apply_lanes_per_tile(ws.nbins, 3 * tile_keys_of(ws));
-    StackTable one = st;
-    one.nf = 1;
+    const bool big = ws.tile_keys == 2 * kPartTileKeys;
+    hipError_t e = hipSuccess;
     switch (variant) {
-        case 0: return launch_probe_stacked(ks, mp, st, ws, res, slots, out, nw, s) == hipSuccess ? 0 : -5;
-        case 1: return launch_bin<true>(ks, mp, ws, slots, s) == hipSuccess ? 0 : -5;
-        case 2: return launch_apply<kApplyStack>(ws, mmax, nullptr, 0, 0, res, st, s) == hipSuccess ? 0 : -5;
-        case 3:
-            if (G == 4) UB_STACK(4, 2, st); else if (G == 8) UB_STACK(8, 2, st); else return -22;
-            break;
-        case 4:
-            if (G == 4) UB_STACK(4, 0, one); else if (G == 8) UB_STACK(8, 0, one); else return -22;
-            break;
-        case 5:
-            return launch_combine(ws, res, slots, n, out, nw, st, s) == hipSuccess ? 0 : -5;
-            break;
-        case 6:
-            if (G == 4) UB_STACK(4, 3, st); else if (G == 8) UB_STACK(8, 3, st); else return -22;
-            break;
-        case 8:
-            if (G == 4) UB_STACKB(4, 0, st, 512); else if (G == 8) UB_STACKB(8, 0, st, 512); else return -22;
-            break;
-        case 10:
-            if (G == 4) UB_STACKB(4, 2, st, 512); else if (G == 8) UB_STACKB(8, 2, st, 512); else return -22;
-            break;
-        case 11:  // image staging only
-            if (G == 8) UB_STACK(8, 4, st); else return -22;
-            break;
-        case 201: UB_STACKD(8, 1); break;
-        case 203: UB_STACKD(8, 3); break;
-        case 204: UB_STACKD(8, 4); break;
-        case 102: UB_STACK(2, 0, st); break;
-        case 104: UB_STACK(4, 0, st); break;
-        case 108: UB_STACK(8, 0, st); break;
-        case 116: UB_STACK(16, 0, st); break;
+        case 0: e = launch_probe_stacked(ks, mp, st, ws, res, slots, out, nw, s); break;
+        case 1: e = launch_bin<true>(ks, mp, ws, slots, s); break;
+        case 2: e = launch_apply<kApplyStack>(ws, mmax, nullptr, 0, 0, res, st, s); break;
+        case 5: e = launch_combine(ws, res, slots, n, out, nw, st, s); break;
+#define UB_SG(G)                                                                                  \
+    case 100 + G:                                                                                 \
+        e = big ? launch_apply_g<kApplyStack, G, 2 * (int)kPartTileKeys>(ws, mmax, nullptr, 0, 0, \
+                                                                        res, st, s)               \
+                : launch_apply_g<kApplyStack, G, (int)kPartTileKeys>(ws, mmax, nullptr, 0, 0,     \
+                                                                    res, st, s);                  \
+        break;
+        UB_SG(4) UB_SG(8) UB_SG(16)
+#undef UB_SG
         default: return -22;
     }
-#undef UB_STACK
-#undef UB_STACKB
-#undef UB_STACKT
-#undef UB_STACKD
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return e == hipSuccess ? 0 : -5;
 }

@@ -53,7 +53,7 @@ def torch_cuda():
 # ---------------------------------------------------------------- build ----
 @pytest.mark.parametrize("m", [1, 2, 31, 32, 33, 64, 65, 256, 1000, 65_537, 512_000, 524_288,
                                1_000_003, 4_194_304, 10_485_761, 167_772_160, 671_088_640,
-                               2**32 - 1])
+                               2**32 - 1, 2**32, 2**32 + 1_000_003, 2**33 - 7])
 @pytest.mark.parametrize("strategy", STRATEGIES, ids=["atomic", "lds", "partition"])
 def test_build_matches_oracle(coracle, m, strategy):
     n = 200_000 if m > 100_000 else 5_000

@@ -196,3 +196,20 @@ def test_binding_refuses_keys_that_are_not_int32():
         bh._out_ptr(np.zeros(8, dtype=np.int32), 16, 8, "out")    # wrong element size
     with pytest.raises(ValueError):
         bh.compact([np.zeros((4, 2), dtype=np.int64)])
+
+
+def test_engine_wide_mod_random_m(fuzz_keys):
+    """mod_wide (2^32 <= m <= 2^46: double-estimated quotient + one exact
+    correction) against the exact remainder, m spread over the whole range
+    and packed near powers of two and near quotient boundaries."""
+    rng = np.random.default_rng(17)
+    ms = np.concatenate([rng.integers(2**32, 2**46 + 1, size=200, dtype=np.uint64),
+                         (np.uint64(1) << rng.integers(32, 47, size=60).astype(np.uint64)) +
+                         rng.integers(-3, 4, size=60).astype(np.int64).astype(np.uint64),
+                         np.array([2**32, 2**32 + 1, 2**32 + 1_000_003, 2**46, 2**46 - 1],
+                                  dtype=np.uint64)])
+    for m in ms.tolist():
+        if not 2**32 <= m <= 2**46:
+            continue
+        assert (bh.host_positions(int(m), fuzz_keys[:3000]) ==
+                np_positions(fuzz_keys[:3000], int(m))).all(), m

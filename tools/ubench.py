@@ -15,12 +15,11 @@ LIB = ctypes.CDLL(os.path.join(ROOT, "cs265-lsm-tree_amd", "lib", "libbloomhip_u
 LIB.ubench_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 LIB.ubench_run.restype = ctypes.c_int
-LIB.ubench_part_bin.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
-                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-LIB.ubench_part_bin.restype = ctypes.c_int
-LIB.ubench_part_apply.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
-                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
-LIB.ubench_part_apply.restype = ctypes.c_int
+LIB.ubench_part_geometry.argtypes = [ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p]
+LIB.ubench_part_geometry.restype = ctypes.c_int
+LIB.ubench_part.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
+                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+LIB.ubench_part.restype = ctypes.c_int
 LIB.ubench_stack.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                              ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_void_p] * 6
 LIB.ubench_stack.restype = ctypes.c_int
@@ -43,153 +42,50 @@ def timeit(which, buf, nbytes, m, grid, block, iters, reps=5):
     return a.elapsed_time(b) / reps
 
 
-def part_ablation(n=16_777_216, bpe=10.0):
-    """Pass 1 of the partition build (C2 by default) with phases removed, and
-    pass-2 variants on its output."""
-    sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
-    import bloomhip as bh
-    keys = torch.from_numpy(bh.gen_puts(13141, n)).cuda()
-    m = bh.m_bits(n, bpe)
-    ntiles = (keys.numel() + 4095) // 4096
-    nbins = 4096  # upper bound for the run-start table
-    pos = torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda")
-    rs = torch.empty(ntiles * (nbins + 1) * 2, dtype=torch.int32, device="cuda")  # both layouts
+def _events(fn, reps):
     s = torch.cuda.current_stream()
-    names = {0: "product", 1: "no tile store", 2: "no scatter/store", 3: "hash only",
-             4: "full, column runs", 5: "full, row runs", 6: "transpose only"}
-    for ab in range(7):
-        for _ in range(3):
-            LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(),
-                                rs.data_ptr(), s.cuda_stream)
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(s)
-        for _ in range(10):
-            LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(),
-                                rs.data_ptr(), s.cuda_stream)
-        b.record(s)
-        torch.cuda.synchronize()
-        print(json.dumps({"op": "k_part_bin", "ablate": names[ab],
-                          "us": round(a.elapsed_time(b) / 10 * 1e3, 2)}), flush=True)
-    # pass 2 variants on the positions of a full pass 1 (sub-segment order,
-    # then segment order)
-    words = torch.zeros((m + 63) // 64 * 2, dtype=torch.int32, device="cuda")
-    for layout, ab in (("sub-sorted", 0),):
-        LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(), rs.data_ptr(),
-                            s.cuda_stream)
-        torch.cuda.synchronize()
-        for batch in (0, 4, 8, 16, 402, 404, 408, 416, 502, 504, 508, 516, 0):
-            for _ in range(2):
-                rc = LIB.ubench_part_apply(batch, pos.data_ptr(), rs.data_ptr(), keys.numel(), m,
-                                           words.data_ptr(), s.cuda_stream)
-                assert rc == 0, (batch, rc)
-            torch.cuda.synchronize()
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(s)
-            for _ in range(10):
-                LIB.ubench_part_apply(batch, pos.data_ptr(), rs.data_ptr(), keys.numel(), m,
-                                      words.data_ptr(), s.cuda_stream)
-            b.record(s)
-            torch.cuda.synchronize()
-            print(json.dumps({"op": "k_part_apply", "n": n, "variant": batch,
-                              "us": round(a.elapsed_time(b) / 10 * 1e3, 2)}), flush=True)
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
 
 
-def part_stagger(n=16_777_216, bpe=10.0):
-    """Pass 1 (C2) as the product launches it (0), with one workgroup per CU
-    (7), and with the second half of the grid started late (8..10)."""
+def part_phases(n=16_777_216, bpe=10.0, reps=50):
+    """The product's partition build (C2 by default) by pass, and pass 2 with
+    each lane count G (ubench_part)."""
+    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
     import bloomhip as bh
     keys = torch.from_numpy(bh.gen_puts(13141, n)).cuda()
     m = bh.m_bits(n, bpe)
-    ntiles = (keys.numel() + 4095) // 4096
-    pos = torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda")
-    rs = torch.empty(ntiles * 4097 * 2, dtype=torch.int32, device="cuda")
+    geo = np.zeros(4, dtype=np.uint64)
+    assert LIB.ubench_part_geometry(n, m, geo.ctypes.data) == 0
+    nbins, seg_bits, tk, ntiles = (int(x) for x in geo)
+    pos = torch.empty(ntiles * tk, dtype=torch.int64, device="cuda")
+    runs = torch.empty(ntiles * (nbins + 1) * 2, dtype=torch.int32, device="cuda")
+    words = torch.zeros((m + 63) // 64 * 2, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
-    names = {0: "product", 7: "one workgroup per CU", 8: "stagger 8K cycles",
-             9: "stagger 16K cycles", 10: "stagger 24K cycles"}
-    ref = None
-    for ab in (0, 7, 8, 9, 10, 0):
-        for _ in range(3):
-            assert LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(),
-                                       rs.data_ptr(), s.cuda_stream) == 0
-        torch.cuda.synchronize()
-        same = None
-        if ab in (0, 8):
-            h = (pos.sum().item(), rs[:ntiles * 257].sum().item())
-            ref = h if ref is None else ref
-            same = h == ref
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(s)
-        for _ in range(20):
-            LIB.ubench_part_bin(ab, keys.data_ptr(), keys.numel(), m, pos.data_ptr(),
-                                rs.data_ptr(), s.cuda_stream)
-        b.record(s)
-        torch.cuda.synchronize()
-        print(json.dumps({"op": "k_part_bin", "variant": names[ab], "same_output": same,
-                          "us": round(a.elapsed_time(b) / 20 * 1e3, 2)}), flush=True)
+
+    def run(v):
+        rc = LIB.ubench_part(v, keys.data_ptr(), n, m, pos.data_ptr(), runs.data_ptr(),
+                             words.data_ptr(), s.cuda_stream)
+        assert rc == 0, (v, rc)
+    names = {0: "pass 1", 1: "pass 2 (product G)", 4: "pass 2 G=4", 8: "pass 2 G=8",
+             16: "pass 2 G=16", 32: "pass 2 G=32"}
+    run(0)
+    for v, name in names.items():
+        ms = _events(lambda: run(v), reps)
+        print(json.dumps({"op": "partition build", "n": n, "m": m, "nbins": nbins,
+                          "seg_bits": seg_bits, "tile_keys": tk, "phase": name,
+                          "us": round(ms * 1e3, 1)}), flush=True)
 
 
-def overlap(n=16_777_216, bpe=10.0):
-    """Does pass 1 of one half-batch overlap pass 2 of the other on two
-    streams?  Times bin(A) apply(A) bin(B) apply(B) on one stream against
-    bin(A); {bin(B) || apply(A)}; apply(B), for both pass-1 grids."""
-    sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
-    import bloomhip as bh
-    m = bh.m_bits(n, bpe)
-    half = n // 2
-    keys = torch.from_numpy(bh.gen_puts(13141, n)).cuda()
-    ka, kb = keys[:half], keys[half:]
-    ntiles = (half + 4095) // 4096
-    bufs = []
-    for _ in range(2):
-        bufs.append((torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda"),
-                     torch.empty(ntiles * 4097 * 2, dtype=torch.int32, device="cuda")))
-    words = torch.zeros((m + 63) // 64 * 2, dtype=torch.int32, device="cuda")
-    s1 = torch.cuda.current_stream()
-    s2 = torch.cuda.Stream()
 
-    def binp(variant, k, b, s):
-        rc = LIB.ubench_part_bin(variant, k.data_ptr(), k.numel(), m, b[0].data_ptr(),
-                                 b[1].data_ptr(), s.cuda_stream)
-        assert rc == 0, rc
-
-    def apply(k, b, s):
-        rc = LIB.ubench_part_apply(0, b[0].data_ptr(), b[1].data_ptr(), k.numel(), m,
-                                   words.data_ptr(), s.cuda_stream)
-        assert rc == 0, rc
-
-    def seq(variant):
-        binp(variant, ka, bufs[0], s1)
-        apply(ka, bufs[0], s1)
-        binp(variant, kb, bufs[1], s1)
-        apply(kb, bufs[1], s1)
-
-    def ovl(variant):
-        binp(variant, ka, bufs[0], s1)
-        e = torch.cuda.Event()
-        e.record(s1)
-        s2.wait_event(e)
-        apply(ka, bufs[0], s2)
-        binp(variant, kb, bufs[1], s1)
-        e2 = torch.cuda.Event()
-        e2.record(s2)
-        s1.wait_event(e2)
-        apply(kb, bufs[1], s1)
-
-    for name, fn, v in (("seq grid2x", seq, 4), ("ovl grid2x", ovl, 4), ("seq grid1x", seq, 7),
-                        ("ovl grid1x", ovl, 7)):
-        for _ in range(3):
-            fn(v)
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(s1)
-        for _ in range(20):
-            fn(v)
-        b.record(s1)
-        torch.cuda.synchronize()
-        print(json.dumps({"op": "half-batch pipeline", "mode": name,
-                          "us": round(a.elapsed_time(b) / 20 * 1e3, 2)}), flush=True)
 
 
 def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
@@ -213,12 +109,13 @@ def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
     nb, sb = ctypes.c_uint64(), ctypes.c_uint64()
     assert LIB.ubench_stack_geometry(nf, msa.ctypes.data, ctypes.byref(nb), ctypes.byref(sb)) == 0
     n = gets.size
-    ntiles = (n + 4095) // 4096
+    tk = 8192 if nb.value > 256 else 4096
+    ntiles = (n + tk - 1) // tk
     dk = torch.from_numpy(gets).cuda()
-    pos = torch.empty(ntiles * 12288, dtype=torch.int32, device="cuda")
+    pos = torch.empty(ntiles * tk, dtype=torch.int64, device="cuda")
     runs = torch.empty(2 * ntiles * (nb.value + 1), dtype=torch.int32, device="cuda")
-    res = torch.empty(ntiles * 12288, dtype=torch.uint8, device="cuda")
-    slots = torch.empty(ntiles * 12288, dtype=torch.int16, device="cuda")
+    res = torch.empty(ntiles * tk * 3, dtype=torch.uint8, device="cuda")
+    slots = torch.empty(ntiles * tk * 3, dtype=torch.int16, device="cuda")
     out = torch.empty(nf * ((n + 63) // 64), dtype=torch.int64, device="cuda")
     s = torch.cuda.current_stream()
 
@@ -227,13 +124,8 @@ def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
                                 runs.data_ptr(), res.data_ptr(), slots.data_ptr(), out.data_ptr(),
                                 s.cuda_stream)
     assert run(0) == 0
-    names = {0: "all three", 1: "pass 1 (+slots, +transpose)", 2: "pass 2",
-             3: "pass 2, no result stores", 4: "pass 2, member 0 image only", 5: "combine",
-             6: "pass 2, non-temporal position loads",
-             102: "pass 2 G=2", 104: "pass 2 G=4", 108: "pass 2 G=8", 116: "pass 2 G=16",
-             8: "pass 2, 512-thread blocks", 10: "pass 2, 512-thread blocks, no result stores",
-             11: "pass 2, image staging only", 201: "pass 2 G=8 depth 1",
-             203: "pass 2 G=8 depth 3", 204: "pass 2 G=8 depth 4"}
+    names = {0: "all three", 1: "pass 1 (+slots, +transpose)", 2: "pass 2", 5: "combine",
+             104: "pass 2 G=4", 108: "pass 2 G=8", 116: "pass 2 G=16"}
     for v in names:
         if run(v) != 0:
             continue
@@ -271,18 +163,12 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "stack":
         stack_ablation()
         return stack_ablation((0, 1, 2, 3))
-    if len(sys.argv) > 1 and sys.argv[1] == "isa":
-        return isa_rates()
-    if len(sys.argv) > 1 and sys.argv[1] == "stagger":
-        return part_stagger()
     if len(sys.argv) > 1 and sys.argv[1] == "part":
-        return part_ablation()
+        return part_phases()
     if len(sys.argv) > 1 and sys.argv[1] == "part_c5":
-        return part_ablation(67_108_864, 10.0)
-    if len(sys.argv) > 1 and sys.argv[1] == "overlap":
-        return overlap()
+        return part_phases(67_108_864, 10.0, 20)
     if len(sys.argv) > 1 and sys.argv[1] == "part_c4":
-        return part_ablation(268_435_456, 12.0)
+        return part_phases(268_435_456, 12.0, 5)
     grid, block = 2048, 256
     threads = grid * block
     out = []
