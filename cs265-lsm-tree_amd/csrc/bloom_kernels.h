@@ -79,12 +79,14 @@ constexpr uint32_t kEntryBits = 21;
 constexpr uint32_t kEntryMask = (1u << kEntryBits) - 1u;
 static_assert(kStackMaxBits <= (1u << kEntryBits), "segment offsets fit an entry");
 
-// p -> segment: q = p >> shift (< kPartMaxSub), b = ident ? q : mulhi(q, magic).
+// p -> segment, branch-free: x = p >> (sub_shift - 1) (< 2 * kPartMaxSub),
+// b = mulhi(x, magic) = (x >> 1) / group.  magic = ceil(2^31 / group) (2^31
+// for group 1), checked exact for every x < 2 * nsub when planned.
 struct SegMap {
-    uint32_t shift;
-    uint32_t magic;  // ceil(2^32 / group), checked exact for every q < nsub
-    uint32_t ident;  // group == 1
+    uint32_t shift;  // sub_shift - 1
+    uint32_t magic;
     uint32_t nbins;
+    uint32_t pad;
 };
 
 struct PartitionWorkspace {
@@ -102,7 +104,7 @@ struct PartitionWorkspace {
 };
 
 inline SegMap seg_map_of(const PartitionWorkspace &ws) {
-    return SegMap{ws.sub_shift, ws.magic, ws.group == 1 ? 1u : 0u, (uint32_t)ws.nbins};
+    return SegMap{ws.sub_shift - 1, ws.magic, (uint32_t)ws.nbins, 0};
 }
 
 // Keys per pass-1 tile for a batch sorted into nbins segments: short runs

@@ -191,11 +191,11 @@ __device__ __forceinline__ size_t part_tile(size_t k, size_t ntiles) {
 }
 
 // The segment of position p (SegMap: a shift, then an exact multiply-high
-// division by the group, checked on the host for every shifted value).
+// division, checked on the host for every shifted value): two instructions,
+// no branch.
 template <typename P>
 __device__ __forceinline__ uint32_t seg_of(P p, const SegMap &sm) {
-    const uint32_t q = (uint32_t)(p >> sm.shift);
-    return sm.ident ? q : __umulhi(q, sm.magic);
+    return __umulhi((uint32_t)(p >> sm.shift), sm.magic);
 }
 
 // Rank bits of a (segment, rank) register: ranks < 3 * 8192 < 2^15.
@@ -1101,17 +1101,14 @@ int device_cu_count() {
     return cus[dev];
 }
 
-// The exact multiply-high divisor of SegMap: ceil(2^32 / g), accepted only
-// when mulhi(q, magic) == q / g for every q < nsub (checked here, once per
-// plan: nsub <= kPartMaxSub).
+// The multiply-high divisor of SegMap: magic = ceil(2^31 / g), accepted only
+// when mulhi(x, magic) == (x >> 1) / g for every x < 2 * nsub (checked here,
+// once per plan: nsub <= kPartMaxSub).  g = 1 gives 2^31, i.e. x >> 1.
 static bool seg_magic(uint32_t g, uint32_t nsub, uint32_t *magic) {
-    if (g <= 1) {
-        *magic = 0;
-        return true;
-    }
-    const uint32_t M = (uint32_t)(((1ull << 32) + g - 1) / g);
-    for (uint32_t q = 0; q < nsub; q++)
-        if ((uint32_t)(((uint64_t)q * M) >> 32) != q / g) return false;
+    if (g == 0) return false;
+    const uint32_t M = (uint32_t)(((1ull << 31) + g - 1) / g);
+    for (uint32_t x = 0; x < 2 * nsub; x++)
+        if ((uint32_t)(((uint64_t)x * M) >> 32) != (x >> 1) / g) return false;
     *magic = M;
     return true;
 }

@@ -27,6 +27,11 @@ for s in ${STEPS//,/ }; do
     bench) run bench 600 python bench.py || exit 1 ;;
     bench_quick) run bench_quick 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline || exit 1 ;;
     bench_c4) run bench_c4 400 python bench.py --workload c4 --steps 5 --warmup 1 --no-extras --no-cpu-baseline || exit 1 ;;
+    bench_c4w) run bench_c4w 400 python bench.py --workload c4w --steps 5 --warmup 1 --no-extras --no-cpu-baseline || exit 1 ;;
+    ub_part) run ub_part 300 python tools/ubench.py part || exit 1 ;;
+    ub_part_c5) run ub_part_c5 300 python tools/ubench.py part_c5 || exit 1 ;;
+    ub_part_c4) run ub_part_c4 300 python tools/ubench.py part_c4 || exit 1 ;;
+    ub_stack) run ub_stack 300 python tools/ubench.py stack || exit 1 ;;
     bench_c5) run bench_c5 400 python bench.py --workload c5 --steps 20 --warmup 3 --no-extras --no-cpu-baseline || exit 1 ;;
     stats_c2) run stats_c2 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c2" -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline --prewarm-s 0 || exit 1 ;;
     stats_c3) run stats_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3" -o run --output-format csv -- python tools/probe_prof.py auto 30 || exit 1 ;;

@@ -6,6 +6,7 @@ correction of MI355X_MICROARCH.md, HBM section: it tallies 128-B requests at
 workload's own build; smaller grids are the tests' warm-up builds).
 
 Usage: pmc_traffic.py WORKLOAD TAG  -> profiles/pmc_WORKLOAD.json
+(TAG = the tools/gpu_steps.sh tag whose pmc_W step wrote gpurun_out/TAG/pmc_W_*)
 """
 import json
 import os
@@ -24,22 +25,22 @@ def per_kernel(d):
     for key, ctrs in pmc_summary.main(d).items():
         name, grid = key.rsplit(" grid=", 1)
         base = name.split("<")[0]
-        if base not in BUILD_KERNELS or "<true" in name:  # PROBE / SLOTS variants
+        if base not in BUILD_KERNELS:
             continue
         if base == "k_part_apply" and not name.startswith("k_part_apply<0"):  # probe modes
             continue
         if base == "k_part_bin":
             targs = [a.strip() for a in name.split("<", 1)[1].split(">")[0].split(",")]
-            if len(targs) > 2 and targs[2] == "true":
-                continue  # SLOTS (probe) variant: k_part_bin<LAYOUT, ABLATE, SLOTS, COLS, TB>
+            if len(targs) > 1 and targs[1] == "true":
+                continue  # SLOTS (probe) variant: k_part_bin<LAYOUT, SLOTS, COLS, TB, WIDE>
         if base not in best or int(grid) > best[base][0]:
             best[base] = (int(grid), name, ctrs)
     return best
 
 
 def main(w, tag):
-    f = per_kernel(os.path.join(ROOT, "gpurun_out", f"pmc_{w}_{tag}_FETCH_SIZE"))
-    wr = per_kernel(os.path.join(ROOT, "gpurun_out", f"pmc_{w}_{tag}_WRITE_SIZE"))
+    f = per_kernel(os.path.join(ROOT, "gpurun_out", tag, f"pmc_{w}_FETCH_SIZE"))
+    wr = per_kernel(os.path.join(ROOT, "gpurun_out", tag, f"pmc_{w}_WRITE_SIZE"))
     kernels = {}
     total = 0
     for base in BUILD_KERNELS:
@@ -50,9 +51,12 @@ def main(w, tag):
         kernels[base] = {"name": f[base][1], "grid": f[base][0], "fetch_bytes": int(fetch),
                          "write_bytes": int(write)}
         total += fetch + write
+    sys.path.insert(0, ROOT)
+    from bench import kernel_source_sha
     out = {"workload": w, "round": tag, "hbm_bytes_per_build": int(total), "kernels": kernels,
+           "kernel_source_sha": kernel_source_sha(),
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
-                     "(tools/gpu_prof.sh); FETCH_SIZE x2 (gfx950); KiB -> bytes; median per "
+                     "(tools/gpu_steps.sh pmc_W); FETCH_SIZE x2 (gfx950); KiB -> bytes; median per "
                      "dispatch of each build kernel's largest grid, summed over the build"}
     path = os.path.join(ROOT, "profiles", f"pmc_{w}.json")
     json.dump(out, open(path, "w"), indent=1)
