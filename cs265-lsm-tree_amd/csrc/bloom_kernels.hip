@@ -198,8 +198,14 @@ __device__ __forceinline__ uint32_t seg_of(P p, const SegMap &sm) {
     return __umulhi((uint32_t)(p >> sm.shift), sm.magic);
 }
 
-// Rank bits of a (segment, rank) register: ranks < 3 * 8192 < 2^15.
-constexpr uint32_t kRankBits = 15;
+// A pass-1 histogram bin b starts at b << kBinShift and counts in steps of 4,
+// so the rank atomic returns (b << kBinShift) + 4 * rank: (that >> 17) is the
+// byte address 4b of the bin's offset, (that & 0x1FFFF) the rank's byte
+// offset (4 * rank < 4 * 3 * 8192 < 2^17), and no VALU touches the atomic's
+// result before the scatter (its wait sits at the barrier).  After the scan
+// the bins hold BYTE offsets into the sorted image.
+constexpr uint32_t kBinShift = 19;  // 8192 segments << 19 < 2^32
+constexpr uint32_t kRankByteMask = (1u << 17) - 1u;
 
 // Outputs: pos_out[tile * kTileKeys ..] (u64), the tile's entries sorted by
 // segment, packed three per u64; where segment b's run of the tile starts
@@ -215,7 +221,8 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
     constexpr int kTilePos = 3 * kTileKeys;
     constexpr int kMaxB = TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
     constexpr int kScanPer = (kMaxB + 1 + TB - 1) / TB;  // scan entries per thread, at most
-    static_assert(kTilePos < (1 << kRankBits), "ranks fit their field");
+    static_assert(4 * kTilePos <= (1 << 17) && ((uint64_t)(kMaxB - 1) << kBinShift) < (1ull << 32),
+                  "packed rank fields (bin nbins, never incremented, may wrap to 0)");
     // static LDS even for the 96 KiB of an 8192-key tile (gfx950 takes it);
     // dynamic LDS or a pointer to it made the compiler spill registers here
     __shared__ __attribute__((aligned(16))) uint32_t s_sorted[kTilePos];
@@ -238,13 +245,13 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
         const size_t tile0 = tile * kTileKeys;
         const int tile_keys = FULL ? (int)kTileKeys : (int)min((size_t)kTileKeys, ks.n - tile0);
         auto live = [&](int j) { return FULL || j * TB + tid < tile_keys; };
-        for (int b = tid; b <= nb; b += TB) s_hist[b] = 0;
+        for (int b = tid; b <= nb; b += TB) s_hist[b] = (uint32_t)b << kBinShift;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
 
         // 1. positions -> (segment, rank in segment) and the entry; the ranks
         //    are not consumed before the barrier, so all 24 LDS atomics of a
         //    thread stay in flight behind the hashing.
-        uint32_t br[kPartKPT * 3];   // segment << kRankBits | rank
+        uint32_t br[kPartKPT * 3];   // (segment << kBinShift) + 4 * rank
         uint32_t ent[kPartKPT * 3];  // low kEntryBits bits of the position
 #pragma unroll
         for (int j = 0; j < kPartKPT; j++) {
@@ -263,7 +270,7 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
                         b = seg_of(p, sm);
                         ent[3 * j + h] = p & kEntryMask;
                     }
-                    br[3 * j + h] = (b << kRankBits) | atomicAdd(&s_hist[b], 1u);
+                    br[3 * j + h] = atomicAdd(&s_hist[b], 4u);
                 }
             } else {
 #pragma unroll
@@ -274,12 +281,12 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
 
         // 2. exclusive scan of the nbins+1 counts (the extra slot is 0 and
         //    receives the tile total); thread t owns [t*per, t*per + per).
-        uint32_t local[kScanPer];
+        uint32_t local[kScanPer];  // 4 * count of bin b
         uint32_t tsum = 0;
 #pragma unroll
         for (int q = 0; q < kScanPer; q++) {
             const int b = tid * per + q;
-            local[q] = (q < per && b <= nb) ? s_hist[b] : 0u;
+            local[q] = (q < per && b <= nb) ? s_hist[b] - ((uint32_t)b << kBinShift) : 0u;
             tsum += local[q];
         }
         uint32_t incl = tsum;
@@ -302,28 +309,31 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
         }
         lds_barrier();
         if constexpr (COLS) {
-            for (int b = tid; b <= nb; b += TB) runs[(size_t)b * ntiles + tile] = s_hist[b];
+            for (int b = tid; b <= nb; b += TB) runs[(size_t)b * ntiles + tile] = s_hist[b] >> 2;
         } else {
             uint32_t *row = runs + tile * (size_t)(nb + 1);
-            for (int b = tid; b <= nb; b += TB) row[b] = s_hist[b];
+            for (int b = tid; b <= nb; b += TB) row[b] = s_hist[b] >> 2;
         }
         if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
 
         // 3. scatter into the LDS image sorted by segment, one hash at a time:
         //    its kPartKPT offset reads first (one wait), then the writes.
+        //    Byte addresses throughout (the histogram holds byte offsets).
+        const char *hist_b = reinterpret_cast<const char *>(s_hist);
+        char *sorted_b = reinterpret_cast<char *>(s_sorted);
 #pragma unroll
         for (int h = 0; h < 3; h++) {
-            uint32_t slot[kPartKPT];
+            uint32_t slot[kPartKPT];  // byte offset in the sorted image
 #pragma unroll
             for (int j = 0; j < kPartKPT; j++)
-                slot[j] = s_hist[br[3 * j + h] >> kRankBits] +
-                          (br[3 * j + h] & ((1u << kRankBits) - 1u));
+                slot[j] = *reinterpret_cast<const uint32_t *>(hist_b + (br[3 * j + h] >> 17)) +
+                          (br[3 * j + h] & kRankByteMask);
 #pragma unroll
             for (int j = 0; j < kPartKPT; j++) {
                 if (live(j)) {
-                    s_sorted[slot[j]] = ent[3 * j + h];
+                    *reinterpret_cast<uint32_t *>(sorted_b + slot[j]) = ent[3 * j + h];
                     if constexpr (SLOTS)
-                        slots[(tile * 3 + h) * kTileKeys + j * TB + tid] = (uint16_t)slot[j];
+                        slots[(tile * 3 + h) * kTileKeys + j * TB + tid] = (uint16_t)(slot[j] >> 2);
                 }
             }
         }
@@ -515,8 +525,12 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             }
         }
     };
+    // Vector vi of tile t; lanes past the tile's last vector load that one
+    // but keep their own vi, so none of its entries counts for them (a
+    // clamped index would make up to G-1 lanes OR the same words, and those
+    // same-address LDS atomics serialise the segments at a tile's end).
     auto load = [&](int t, uint32_t vi) -> uint4 {
-        return reinterpret_cast<const uint4 *>(pos + (size_t)t * TILE_KEYS)[vi];
+        return reinterpret_cast<const uint4 *>(pos + (size_t)t * TILE_KEYS)[min(vi, kLastVec)];
     };
     // The six entries of vector vi of tile t; run = [r.x, r.y).
     auto apply6 = [&](const uint4 &v, int t, uint32_t vi, const uint2 &r) {
@@ -525,12 +539,23 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                                __builtin_amdgcn_alignbit(v.w, v.z, 21) & kEntryMask, v.w >> 10};
         const uint32_t i0 = 6 * vi - r.x, len = r.y - r.x;  // entry k is in the run iff i0 + k < len
         if constexpr (!PROBE) {
+            // Branch-free: the run's entries among the six form the 6-bit
+            // mask vm; an entry outside the run ORs 0.  The word's LDS byte
+            // address is ((e - base) mod 2^21) / 32 * 4 (the segment image
+            // starts at LDS address 0: the kernel has no static LDS) and the
+            // bit index the low 5 bits of e - base, which the shift takes as
+            // they are.
+            const int s0 = (int)(6 * vi) - (int)r.x;          // entry 0's place in the run
+            const int lo = max(-s0, 0), hi = min(max((int)r.y - (int)(6 * vi), 0), 6);
+            const uint32_t vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
 #pragma unroll
             for (int k = 0; k < 6; k++) {
-                if (i0 + k < len) {
-                    const uint32_t o = (e[k] - base21) & kEntryMask;
-                    atomicOr(&seg[o >> 5], 1u << (o & 31));
-                }
+                const uint32_t d = e[k] - base21;
+                const uint32_t addr = (d >> 3) & ((kEntryMask >> 3) & ~3u);
+                const uint32_t bit = __builtin_amdgcn_ubfe(vm, k, 1) << (d & 31);
+                __attribute__((address_space(3))) uint32_t *w =
+                    (__attribute__((address_space(3))) uint32_t *)(size_t)addr;
+                __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         } else {
             uint32_t bits[6], mask = 0;
@@ -578,7 +603,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) {
             t[d] = min(j * kBatchTiles + d * kTPI + tl, ntiles - 1);
-            vi[d] = min(r[d].x / 6u + sub, kLastVec);
+            vi[d] = r[d].x / 6u + sub;
             v[d] = load(t[d], vi[d]);
         }
         uint2 rn[DEPTH];
@@ -588,10 +613,8 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         for (int d = 0; d < DEPTH; d++) apply6(v[d], t[d], vi[d], r[d]);
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) {
-            for (uint32_t vn = r[d].x / 6u + sub + G; __ballot(6 * vn < r[d].y) != 0; vn += G) {
-                const uint32_t vc = min(vn, kLastVec);
-                apply6(load(t[d], vc), t[d], vc, r[d]);
-            }
+            for (uint32_t vn = r[d].x / 6u + sub + G; __ballot(6 * vn < r[d].y) != 0; vn += G)
+                apply6(load(t[d], vn), t[d], vn, r[d]);
         }
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) r[d] = rn[d];

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "bloom_kernels.hip"  // the product kernels, for ablation timing builds
 
 using namespace bloomhip;

@@ -5,7 +5,8 @@ import collections
 import re
 import sys
 
-S = "cs265-lsm-tree_amd/lib/obj/bloom_kernels-hip-amdgcn-amd-amdhsa-gfx950.s"
+import os
+S = os.environ.get("ISA_S", "cs265-lsm-tree_amd/lib/obj/bloom_kernels-hip-amdgcn-amd-amdhsa-gfx950.s")
 L = open(S).read().splitlines()
 want, min_valu = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 50
 i = next(k for k, l in enumerate(L) if re.match(r"^_Z\S*: ;", l) and want in l.split(":")[0])

@@ -6,7 +6,7 @@ import re
 import subprocess
 import sys
 
-path = "cs265-lsm-tree_amd/lib/obj/resource_usage.txt"
+path = sys.argv[2] if len(sys.argv) > 2 else "cs265-lsm-tree_amd/lib/obj/resource_usage.txt"
 flt = sys.argv[1] if len(sys.argv) > 1 else ""
 cur, rows = None, []
 for line in open(path):

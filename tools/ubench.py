@@ -75,8 +75,8 @@ def part_phases(n=16_777_216, bpe=10.0, reps=50):
         rc = LIB.ubench_part(v, keys.data_ptr(), n, m, pos.data_ptr(), runs.data_ptr(),
                              words.data_ptr(), s.cuda_stream)
         assert rc == 0, (v, rc)
-    names = {0: "pass 1", 1: "pass 2 (product G)", 4: "pass 2 G=4", 8: "pass 2 G=8",
-             16: "pass 2 G=16", 32: "pass 2 G=32"}
+    names = {0: "pass 1", 1: "pass 2 (product G)", 4: "pass 2 G=4",
+             8: "pass 2 G=8", 16: "pass 2 G=16", 32: "pass 2 G=32"}
     run(0)
     for v, name in names.items():
         ms = _events(lambda: run(v), reps)
