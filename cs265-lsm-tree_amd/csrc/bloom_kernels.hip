@@ -20,6 +20,10 @@
 //               the segment out with coalesced stores.  No global atomics.
 #include "bloom_kernels.h"
 
+#ifndef BH_XP_APPLY
+#define BH_XP_APPLY 0  // experiment selector (ubench builds only)
+#endif
+
 #include <stdlib.h>
 
 namespace bloomhip {
@@ -423,12 +427,14 @@ constexpr int kApplyDepth = 2;  // lane-group loads per wave per batch
 
 // Lanes per tile for pass 2, from the average run length L = tile entries /
 // nbins: a step reads 6G entries of a tile (G lanes x one 16-B vector);
-// runs longer than a step finish in the wave-uniform tail loop.
+// runs longer than a step finish in the wave-uniform tail loop.  Measured
+// (tools/ubench.py part*, G x depth sweep): G = 4 wins from runs of 8 (C4)
+// to 48 entries (C2, C5): C2 38 us vs 66 at G = 8 and 47 at G = 2.
 inline int apply_lanes_per_tile(size_t nbins, size_t tile_pos = kPartTilePos) {
     const size_t L = tile_pos / (nbins ? nbins : 1);
-    if (L < 16) return 4;
-    if (L < 144) return 8;
-    if (L < 288) return 16;
+    if (L < 96) return 4;
+    if (L < 192) return 8;
+    if (L < 384) return 16;
     return 32;
 }
 
@@ -538,6 +544,17 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                                v.y >> 10,        v.z & kEntryMask,
                                __builtin_amdgcn_alignbit(v.w, v.z, 21) & kEntryMask, v.w >> 10};
         const uint32_t i0 = 6 * vi - r.x, len = r.y - r.x;  // entry k is in the run iff i0 + k < len
+#if BH_XP_APPLY == 1
+        if constexpr (!PROBE) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                if (i0 + k < len) {
+                    const uint32_t o = (e[k] - base21) & kEntryMask;
+                    atomicOr(&seg[o >> 5], 1u << (o & 31));
+                }
+            }
+        } else
+#endif
         if constexpr (!PROBE) {
             // Branch-free: the run's entries among the six form the 6-bit
             // mask vm; an entry outside the run ORs 0.  The word's LDS byte
@@ -1279,12 +1296,12 @@ hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const Partiti
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
-template <int MODE, int G, int TK>
+template <int MODE, int G, int TK, int DEPTH = kApplyDepth>
 hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                           uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                           hipStream_t stream) {
     static const bool attr_set = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<MODE, G, TK>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<MODE, G, TK, kApplyBlock, DEPTH>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kStackMaxBits / 8));
         return true;
@@ -1292,7 +1309,7 @@ hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *wo
     (void)attr_set;
     const size_t lds = (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
     if (lds > kStackMaxBits / 8) return hipErrorInvalidValue;
-    k_part_apply<MODE, G, TK><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
+    k_part_apply<MODE, G, TK, kApplyBlock, DEPTH><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
         res, st);
     return hipGetLastError();

@@ -197,6 +197,16 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
         break;
         UB_G(4) UB_G(8) UB_G(16) UB_G(32)
 #undef UB_G
+#define UB_GD(G, D)                                                                               \
+    case 1000 + 10 * G + D:                                                                      \
+        e = big ? launch_apply_g<kApplyBuild, G, 2 * (int)kPartTileKeys, D>(ws, m, words, nw32, 0,  \
+                                                                           nullptr, StackTable{}, s) \
+                : launch_apply_g<kApplyBuild, G, (int)kPartTileKeys, D>(ws, m, words, nw32, 0,        \
+                                                                       nullptr, StackTable{}, s);    \
+        break;
+        UB_GD(1, 1) UB_GD(1, 2) UB_GD(1, 4) UB_GD(2, 1) UB_GD(2, 2) UB_GD(2, 4)
+        UB_GD(4, 1) UB_GD(4, 2) UB_GD(4, 4)
+#undef UB_GD
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

@@ -11,7 +11,8 @@ import sys
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = ctypes.CDLL(os.path.join(ROOT, "cs265-lsm-tree_amd", "lib", "libbloomhip_ubench.so"))
+LIB = ctypes.CDLL(os.environ.get("UBENCH_LIB") or
+                  os.path.join(ROOT, "cs265-lsm-tree_amd", "lib", "libbloomhip_ubench.so"))
 LIB.ubench_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 LIB.ubench_run.restype = ctypes.c_int
@@ -77,6 +78,10 @@ def part_phases(n=16_777_216, bpe=10.0, reps=50):
         assert rc == 0, (v, rc)
     names = {0: "pass 1", 1: "pass 2 (product G)", 4: "pass 2 G=4",
              8: "pass 2 G=8", 16: "pass 2 G=16", 32: "pass 2 G=32"}
+    if os.environ.get("UB_GD"):
+        names = {0: "pass 1", 1: "pass 2 (product G)"}
+        names.update({1000 + 10 * g + d: f"pass 2 G={g} depth={d}"
+                      for g in (1, 2, 4) for d in (1, 2, 4)})
     run(0)
     for v, name in names.items():
         ms = _events(lambda: run(v), reps)
