@@ -86,7 +86,7 @@ struct SegMap {
     uint32_t shift;  // sub_shift - 1
     uint32_t magic;
     uint32_t nbins;
-    uint32_t pad;
+    uint32_t scaled_shift;  // shift + l: the same map on a remainder scaled by 2^l (mod_fast_scaled)
 };
 
 struct PartitionWorkspace {

@@ -156,19 +156,38 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
+// The keys of thread tid in a pass-1 tile: the kPartKPT consecutive keys
+// tile0 + kPartKPT * tid + j, so a whole tile is read as 16-B vectors (two per
+// thread for packed keys, four for entry_t runs); a short last tile by guarded
+// scalar loads.  Which thread hashes which key does not matter to the sort,
+// and the probe's slots are indexed by the key's place in the tile.
 template <int LAYOUT, int TB>
 __device__ __forceinline__ void load_tile_keys(const KeySpan &ks, size_t tile, int tid,
                                                int32_t (&k)[kPartKPT]) {
-    const size_t tile0 = tile * (size_t)(TB * kPartKPT);
+    static_assert(kPartKPT == 8, "two int4 / four entry pairs per thread");
+    const size_t i0 = tile * (size_t)(TB * kPartKPT) + (size_t)kPartKPT * tid;
+    const bool full = (tile + 1) * (size_t)(TB * kPartKPT) <= ks.n;  // uniform per workgroup
+    if constexpr (LAYOUT == KEYS_PACKED) {
+        if (full) {
+            const int4 *v = reinterpret_cast<const int4 *>(ks.base) + i0 / 4;
+            const int4 a = v[0], b = v[1];
+            k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
+            k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
+            return;
+        }
+    } else if constexpr (LAYOUT == KEYS_ENTRY) {  // 16-B aligned entry_t run
+        if (full) {
+            const int4 *v = reinterpret_cast<const int4 *>(ks.base) + i0 / 2;
+            const int4 a = v[0], b = v[1], c = v[2], d = v[3];
+            k[0] = a.x; k[1] = a.z; k[2] = b.x; k[3] = b.z;
+            k[4] = c.x; k[5] = c.z; k[6] = d.x; k[7] = d.z;
+            return;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < kPartKPT; j++) {
-        const size_t i = tile0 + (size_t)j * TB + tid;
-        if (i < ks.n) {
-            if constexpr (LAYOUT == KEYS_PACKED) k[j] = reinterpret_cast<const int32_t *>(ks.base)[i];
-            else k[j] = load_key<LAYOUT>(ks, i);
-        } else {
-            k[j] = 0;
-        }
+        const size_t i = i0 + j;
+        k[j] = i < ks.n ? load_key<LAYOUT>(ks, i) : 0;
     }
 }
 
@@ -204,26 +223,25 @@ __device__ __forceinline__ uint32_t seg_of(P p, const SegMap &sm) {
 
 // A pass-1 histogram bin b starts at b << kBinShift and counts in steps of 4,
 // so the rank atomic returns (b << kBinShift) + 4 * rank: (that >> 17) is the
-// byte address 4b of the bin's offset, (that & 0x1FFFF) the rank's byte
-// offset (4 * rank < 4 * 3 * 8192 < 2^17), and no VALU touches the atomic's
-// result before the scatter (its wait sits at the barrier).  After the scan
-// the bins hold BYTE offsets into the sorted image.
+// byte address 4b of the bin's offset (4 * rank < 4 * 3 * 8192 < 2^17), and
+// no VALU touches the atomic's result before the scatter (its wait sits at the
+// barrier).  After the scan bin b holds its BYTE offset into the sorted image
+// minus b << kBinShift, so bin + rank value is the entry's byte slot.
 constexpr uint32_t kBinShift = 19;  // 8192 segments << 19 < 2^32
-constexpr uint32_t kRankByteMask = (1u << 17) - 1u;
 
 // Outputs: pos_out[tile * kTileKeys ..] (u64), the tile's entries sorted by
 // segment, packed three per u64; where segment b's run of the tile starts
 // (b = 0..nbins): COLS = true: straight into the segment-major table
 // runs[b * ntiles + tile]; COLS = false: into the tile-major
 // runs[tile * (nbins + 1) + b], for k_runs_transpose (large tables).
-template <int LAYOUT, bool SLOTS, bool COLS, int TB, bool WIDE>
-__global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
-                                                    uint64_t *__restrict__ pos_out,
-                                                    uint32_t *__restrict__ runs, SegMap sm,
-                                                    size_t ntiles, uint16_t *__restrict__ slots) {
+template <int LAYOUT, bool SLOTS, bool COLS, int TB, bool WIDE, int MAXB = 0, int MINW = 4>
+__global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
+                                                       uint64_t *__restrict__ pos_out,
+                                                       uint32_t *__restrict__ runs, SegMap sm,
+                                                       size_t ntiles, uint16_t *__restrict__ slots) {
     constexpr int kTileKeys = TB * kPartKPT;
     constexpr int kTilePos = 3 * kTileKeys;
-    constexpr int kMaxB = TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
+    constexpr int kMaxB = MAXB ? MAXB : TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
     constexpr int kScanPer = (kMaxB + 1 + TB - 1) / TB;  // scan entries per thread, at most
     static_assert(4 * kTilePos <= (1 << 17) && ((uint64_t)(kMaxB - 1) << kBinShift) < (1ull << 32),
                   "packed rank fields (bin nbins, never incremented, may wrap to 0)");
@@ -248,7 +266,7 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
         constexpr bool FULL = decltype(full_c)::value;
         const size_t tile0 = tile * kTileKeys;
         const int tile_keys = FULL ? (int)kTileKeys : (int)min((size_t)kTileKeys, ks.n - tile0);
-        auto live = [&](int j) { return FULL || j * TB + tid < tile_keys; };
+        auto live = [&](int j) { return FULL || kPartKPT * tid + j < tile_keys; };
         for (int b = tid; b <= nb; b += TB) s_hist[b] = (uint32_t)b << kBinShift;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
 
@@ -270,9 +288,11 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
                         b = seg_of(p, sm);
                         ent[3 * j + h] = (uint32_t)p & kEntryMask;
                     } else {
-                        const uint32_t p = mod_fast(raw, mp);
-                        b = seg_of(p, sm);
-                        ent[3 * j + h] = p & kEntryMask;
+                        // the remainder still scaled by 2^l: the entry is a
+                        // bit-field of it, and one shift reaches the segment
+                        const uint32_t ru = mod_fast_scaled(raw, mp);
+                        b = __umulhi(ru >> sm.scaled_shift, sm.magic);
+                        ent[3 * j + h] = __builtin_amdgcn_ubfe(ru, mp.l, kEntryBits);
                     }
                     br[3 * j + h] = atomicAdd(&s_hist[b], 4u);
                 }
@@ -307,16 +327,18 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
         for (int q = 0; q < kScanPer; q++) {
             const int b = tid * per + q;
             if (q < per && b <= nb) {
-                s_hist[b] = run;
+                // biased by -(b << kBinShift): bin + rank value = byte slot
+                s_hist[b] = run - ((uint32_t)b << kBinShift);
                 run += local[q];
             }
         }
         lds_barrier();
         if constexpr (COLS) {
-            for (int b = tid; b <= nb; b += TB) runs[(size_t)b * ntiles + tile] = s_hist[b] >> 2;
+            for (int b = tid; b <= nb; b += TB)
+                runs[(size_t)b * ntiles + tile] = (s_hist[b] + ((uint32_t)b << kBinShift)) >> 2;
         } else {
             uint32_t *row = runs + tile * (size_t)(nb + 1);
-            for (int b = tid; b <= nb; b += TB) row[b] = s_hist[b] >> 2;
+            for (int b = tid; b <= nb; b += TB) row[b] = (s_hist[b] + ((uint32_t)b << kBinShift)) >> 2;
         }
         if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
 
@@ -331,13 +353,23 @@ __global__ void __launch_bounds__(TB, 4) k_part_bin(KeySpan ks, ModParams mp,
 #pragma unroll
             for (int j = 0; j < kPartKPT; j++)
                 slot[j] = *reinterpret_cast<const uint32_t *>(hist_b + (br[3 * j + h] >> 17)) +
-                          (br[3 * j + h] & kRankByteMask);
+                          br[3 * j + h];
 #pragma unroll
-            for (int j = 0; j < kPartKPT; j++) {
-                if (live(j)) {
-                    *reinterpret_cast<uint32_t *>(sorted_b + slot[j]) = ent[3 * j + h];
-                    if constexpr (SLOTS)
-                        slots[(tile * 3 + h) * kTileKeys + j * TB + tid] = (uint16_t)(slot[j] >> 2);
+            for (int j = 0; j < kPartKPT; j++)
+                if (live(j)) *reinterpret_cast<uint32_t *>(sorted_b + slot[j]) = ent[3 * j + h];
+            if constexpr (SLOTS) {
+                // key kPartKPT*tid + j's sorted index, one 16-B store per hash
+                uint16_t *sl = slots + (tile * 3 + h) * kTileKeys + kPartKPT * tid;
+                if (FULL) {
+                    uint32_t w[kPartKPT / 2];
+#pragma unroll
+                    for (int q = 0; q < kPartKPT / 2; q++)
+                        w[q] = (slot[2 * q] >> 2) | ((slot[2 * q + 1] >> 2) << 16);
+                    *reinterpret_cast<uint4 *>(sl) = make_uint4(w[0], w[1], w[2], w[3]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kPartKPT; j++)
+                        if (live(j)) sl[j] = (uint16_t)(slot[j] >> 2);
                 }
             }
         }
@@ -1247,32 +1279,73 @@ bool runs_as_columns(const PartitionWorkspace &ws) {
     return ws.ntiles * (ws.nbins + 1) * 4 <= kColumnTableMaxBytes;
 }
 
+// One pass-1 launch: MAXB is the histogram capacity the kernel is compiled
+// for (its scan loop and registers follow it, so a small capacity is cheaper:
+// C2's 256 segments at MAXB 511 run pass 1 in 74.5 us against 87 at 4096,
+// tools/ubench.py part with UB_P1).  Only the packed / entry_t fast paths get
+// the small capacities; strided keys and m >= 2^32 use the largest.
+template <int L, bool SLOTS, int TB, bool W, int MAXB>
+void bin_launch(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                uint32_t *runs, const SegMap &sm, bool cols, unsigned grid, uint16_t *slots,
+                hipStream_t stream) {
+    if (cols)
+        k_part_bin<L, SLOTS, true, TB, W, MAXB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm,
+                                                                        ws.ntiles, slots);
+    else
+        k_part_bin<L, SLOTS, false, TB, W, MAXB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm,
+                                                                         ws.ntiles, slots);
+}
+
+template <int L, bool SLOTS, int TB>
+void bin_launch_fast(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                     uint32_t *runs, const SegMap &sm, bool cols, unsigned grid, uint16_t *slots,
+                     hipStream_t stream) {
+    const size_t nb = ws.nbins;
+    if constexpr (TB >= 1024) {
+        if (nb <= 1023) bin_launch<L, SLOTS, TB, false, 1023>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else if (nb <= 2047) bin_launch<L, SLOTS, TB, false, 2047>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else if (nb <= 4095) bin_launch<L, SLOTS, TB, false, 4095>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else bin_launch<L, SLOTS, TB, false, (int)kPartMaxBinsBig>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+    } else {
+        if (nb <= 511) bin_launch<L, SLOTS, TB, false, 511>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else bin_launch<L, SLOTS, TB, false, (int)kPartMaxBins>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+    }
+}
+
 template <bool SLOTS, int TB>
 hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                          uint16_t *slots, hipStream_t stream) {
-    if (ws.nbins > (TB >= 1024 ? kPartMaxBinsBig : kPartMaxBins)) return hipErrorInvalidValue;
+    constexpr int kCap = TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
+    if (ws.nbins > (size_t)kCap) return hipErrorInvalidValue;
     const unsigned grid = part_bin_grid(ws.ntiles, TB);
     const bool cols = runs_as_columns(ws);
     uint32_t *runs = cols ? ws.run_starts : ws.run_rows;
-    const SegMap sm = seg_map_of(ws);
+    SegMap sm = seg_map_of(ws);
     const bool wide = !mp.fast;
-#define BIN_LAUNCH(L, C, W)                                                                   \
-    k_part_bin<L, SLOTS, C, TB, W><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm, ws.ntiles, \
-                                                            slots)
-#define BIN_LAYOUT(L)                                         \
-    do {                                                      \
-        if (wide) {                                           \
-            if (cols) BIN_LAUNCH(L, true, true);              \
-            else BIN_LAUNCH(L, false, true);                  \
-        } else {                                              \
-            if (cols) BIN_LAUNCH(L, true, false);             \
-            else BIN_LAUNCH(L, false, false);                 \
-        }                                                     \
-    } while (0)
-    if (ks.layout == KEYS_PACKED) BIN_LAYOUT(KEYS_PACKED);
-    else BIN_LAYOUT(KEYS_STRIDED);
-#undef BIN_LAYOUT
-#undef BIN_LAUNCH
+    if (!wide) {  // the fast path shifts the remainder scaled by 2^l
+        sm.scaled_shift = sm.shift + mp.l;
+        if (sm.scaled_shift > 31) {  // m < 2^(32-l) <= 2^shift: every p is in segment 0
+            sm.scaled_shift = 0;
+            sm.magic = 0;
+        }
+    }
+    const bool entry16 =
+        ks.layout == KEYS_ENTRY && (reinterpret_cast<uintptr_t>(ks.base) & 15) == 0;
+    if (wide) {
+        if (ks.layout == KEYS_PACKED)
+            bin_launch<KEYS_PACKED, SLOTS, TB, true, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else if (entry16)
+            bin_launch<KEYS_ENTRY, SLOTS, TB, true, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else
+            bin_launch<KEYS_STRIDED, SLOTS, TB, true, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+    } else {
+        if (ks.layout == KEYS_PACKED)
+            bin_launch_fast<KEYS_PACKED, SLOTS, TB>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else if (entry16)
+            bin_launch_fast<KEYS_ENTRY, SLOTS, TB>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else
+            bin_launch<KEYS_STRIDED, SLOTS, TB, false, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess || cols) return e;
     return launch_runs_transpose(ws, stream);

@@ -110,8 +110,9 @@ inline ModParams make_mod_params(uint64_t m) {
     return p;
 }
 
-// x % m for m < 2^32 (p.fast).  Returns the remainder as u32.
-BH_HD uint32_t mod_fast(uint64_t x, const ModParams &p) {
+// (x % m) << l for m < 2^32 (p.fast): the remainder before the final
+// normalisation shift (callers that take bit-fields of it save that shift).
+BH_HD uint32_t mod_fast_scaled(uint64_t x, const ModParams &p) {
     const uint32_t xh = (uint32_t)(x >> 32), xl = (uint32_t)x;
     const uint64_t y = (uint64_t)xh * p.R + xl;   // < m * 2^32, so u below < dn * 2^32
     const uint64_t u = y << p.l;
@@ -122,8 +123,11 @@ BH_HD uint32_t mod_fast(uint64_t x, const ModParams &p) {
     uint32_t r = u0 - q1 * p.dn;
     if (r > q0) r += p.dn;
     if (r >= p.dn) r -= p.dn;
-    return r >> p.l;
+    return r;
 }
+
+// x % m for m < 2^32 (p.fast).  Returns the remainder as u32.
+BH_HD uint32_t mod_fast(uint64_t x, const ModParams &p) { return mod_fast_scaled(x, p) >> p.l; }
 
 // x % m for 2^32 <= m <= 2^46.  q = trunc(double(x) * (1/m)): x < 2^64 and
 // m >= 2^32 make x/m < 2^32, and the three roundings (x to double, 1/m, the

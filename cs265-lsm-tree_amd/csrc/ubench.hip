@@ -177,7 +177,8 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     const ModParams mp = make_mod_params(m);
     PartitionWorkspace ws{};
     if (!plan_segments(m, device_cu_count(), &ws)) return -34;
-    ws.tile_keys = choose_tile_keys(ws.nbins);
+    const bool half = (variant >= 2004 && variant < 2200 && variant < 2011) || (variant >= 2100 && variant < 2200);  // 2048-key tiles (TB = 256)
+    ws.tile_keys = half ? kPartTileKeys / 2 : choose_tile_keys(ws.nbins);
     ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
     ws.pos = pos;
     ws.run_rows = runs;
@@ -207,6 +208,35 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
         UB_GD(1, 1) UB_GD(1, 2) UB_GD(1, 4) UB_GD(2, 1) UB_GD(2, 2) UB_GD(2, 4)
         UB_GD(4, 1) UB_GD(4, 2) UB_GD(4, 4)
 #undef UB_GD
+        // pass-1 shapes: TB threads x 8 keys, histogram capacity MAXB, MINW
+        // waves per SIMD (register cap), NWG workgroups per CU
+#define UB_P1(V, TB, MAXB, MINW, NWG)                                                            \
+    case V: {                                                                                    \
+        if (ws.nbins > MAXB || ws.tile_keys != TB * kPartKPT) return -22;                        \
+        SegMap sm = seg_map_of(ws);                                                              \
+        sm.scaled_shift = sm.shift + mp.l;                                                       \
+        const unsigned g = (unsigned)std::min<size_t>(ws.ntiles, (size_t)device_cu_count() * NWG); \
+        k_part_bin<KEYS_PACKED, false, true, TB, false, MAXB, MINW>                              \
+            <<<g, TB, 0, s>>>(ks, mp, ws.pos, ws.run_rows, sm, ws.ntiles, nullptr);             \
+        e = hipGetLastError();                                                                   \
+        break;                                                                                   \
+    }
+        UB_P1(2001, 512, 1024, 4, 2) UB_P1(2002, 512, 1024, 5, 3) UB_P1(2003, 512, 1024, 6, 3)
+        UB_P1(2004, 256, 1024, 5, 5) UB_P1(2005, 256, 1024, 6, 5) UB_P1(2006, 256, 1024, 4, 4)
+        UB_P1(2007, 256, 511, 5, 5) UB_P1(2008, 256, 511, 6, 6)
+        UB_P1(2011, 512, 511, 4, 2) UB_P1(2012, 512, 511, 5, 3) UB_P1(2013, 512, 511, 6, 3)
+#undef UB_P1
+        // pass 2 over the 2048-key tiles the TB = 256 variants write (run_rows, columns)
+#define UB_H(G, D)                                                                                \
+    case 2100 + 10 * G + D: {                                                                    \
+        PartitionWorkspace w2 = ws;                                                              \
+        w2.run_starts = ws.run_rows;                                                             \
+        e = launch_apply_g<kApplyBuild, G, (int)kPartTileKeys / 2, D>(w2, m, words, nw32, 0,     \
+                                                                      nullptr, StackTable{}, s); \
+        break;                                                                                   \
+    }
+        UB_H(2, 2) UB_H(4, 1) UB_H(4, 2) UB_H(4, 4) UB_H(8, 2)
+#undef UB_H
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

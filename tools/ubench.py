@@ -78,11 +78,27 @@ def part_phases(n=16_777_216, bpe=10.0, reps=50):
         assert rc == 0, (v, rc)
     names = {0: "pass 1", 1: "pass 2 (product G)", 4: "pass 2 G=4",
              8: "pass 2 G=8", 16: "pass 2 G=16", 32: "pass 2 G=32"}
+    if os.environ.get("UB_P1"):
+        names = {0: "pass 1", 2001: "pass 1 TB512 maxb1024 4w", 2002: "pass 1 TB512 maxb1024 5w 3wg",
+                 2003: "pass 1 TB512 maxb1024 6w 3wg", 2004: "pass 1 TB256 5w 5wg",
+                 2005: "pass 1 TB256 6w 5wg", 2006: "pass 1 TB256 4w 4wg",
+                 2007: "pass 1 TB256 maxb511 5w 5wg", 2008: "pass 1 TB256 maxb511 6w 6wg",
+                 2011: "pass 1 TB512 maxb511 4w", 2012: "pass 1 TB512 maxb511 5w 3wg",
+                 2013: "pass 1 TB512 maxb511 6w 3wg",
+                 2122: "pass 2 (2048-key tiles) G=2 d=2", 2141: "pass 2 (2048) G=4 d=1",
+                 2142: "pass 2 (2048) G=4 d=2", 2144: "pass 2 (2048) G=4 d=4",
+                 2182: "pass 2 (2048) G=8 d=2"}
     if os.environ.get("UB_GD"):
         names = {0: "pass 1", 1: "pass 2 (product G)"}
         names.update({1000 + 10 * g + d: f"pass 2 G={g} depth={d}"
                       for g in (1, 2, 4) for d in (1, 2, 4)})
     run(0)
+    if os.environ.get("UB_P1"):
+        run(0); run(1)
+        ref = words.clone()
+        words.zero_(); run(2006); run(2142)
+        torch.cuda.synchronize()
+        print(json.dumps({"check": "2048-key tiles bitmap == product", "ok": bool(torch.equal(ref, words))}))
     for v, name in names.items():
         ms = _events(lambda: run(v), reps)
         print(json.dumps({"op": "partition build", "n": n, "m": m, "nbins": nbins,
