@@ -502,7 +502,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip probe/e2e legs")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 eight-run leg")
-    ap.add_argument("--prewarm-s", type=float, default=0.3,
+    ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed time-based warm-up before --warmup (0 under profilers)")
     args = ap.parse_args()
 

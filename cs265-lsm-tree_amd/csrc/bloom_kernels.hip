@@ -20,10 +20,6 @@
 //               the segment out with coalesced stores.  No global atomics.
 #include "bloom_kernels.h"
 
-#ifndef BH_XP_APPLY
-#define BH_XP_APPLY 0  // experiment selector (ubench builds only)
-#endif
-
 #include <stdlib.h>
 
 namespace bloomhip {
@@ -576,17 +572,6 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                                v.y >> 10,        v.z & kEntryMask,
                                __builtin_amdgcn_alignbit(v.w, v.z, 21) & kEntryMask, v.w >> 10};
         const uint32_t i0 = 6 * vi - r.x, len = r.y - r.x;  // entry k is in the run iff i0 + k < len
-#if BH_XP_APPLY == 1
-        if constexpr (!PROBE) {
-#pragma unroll
-            for (int k = 0; k < 6; k++) {
-                if (i0 + k < len) {
-                    const uint32_t o = (e[k] - base21) & kEntryMask;
-                    atomicOr(&seg[o >> 5], 1u << (o & 31));
-                }
-            }
-        } else
-#endif
         if constexpr (!PROBE) {
             // Branch-free: the run's entries among the six form the 6-bit
             // mask vm; an entry outside the run ORs 0.  The word's LDS byte

@@ -210,14 +210,15 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
 #undef UB_GD
         // pass-1 shapes: TB threads x 8 keys, histogram capacity MAXB, MINW
         // waves per SIMD (register cap), NWG workgroups per CU
-#define UB_P1(V, TB, MAXB, MINW, NWG)                                                            \
+#define UB_P1(V, TB, MAXB, MINW, NWG) UB_P1R(V, TB, MAXB, MINW, NWG, ws.run_rows)
+#define UB_P1R(V, TB, MAXB, MINW, NWG, RUNS)                                                     \
     case V: {                                                                                    \
         if (ws.nbins > MAXB || ws.tile_keys != TB * kPartKPT) return -22;                        \
         SegMap sm = seg_map_of(ws);                                                              \
         sm.scaled_shift = sm.shift + mp.l;                                                       \
         const unsigned g = (unsigned)std::min<size_t>(ws.ntiles, (size_t)device_cu_count() * NWG); \
         k_part_bin<KEYS_PACKED, false, true, TB, false, MAXB, MINW>                              \
-            <<<g, TB, 0, s>>>(ks, mp, ws.pos, ws.run_rows, sm, ws.ntiles, nullptr);             \
+            <<<g, TB, 0, s>>>(ks, mp, ws.pos, RUNS, sm, ws.ntiles, nullptr);            \
         e = hipGetLastError();                                                                   \
         break;                                                                                   \
     }
@@ -225,7 +226,11 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
         UB_P1(2004, 256, 1024, 5, 5) UB_P1(2005, 256, 1024, 6, 5) UB_P1(2006, 256, 1024, 4, 4)
         UB_P1(2007, 256, 511, 5, 5) UB_P1(2008, 256, 511, 6, 6)
         UB_P1(2011, 512, 511, 4, 2) UB_P1(2012, 512, 511, 5, 3) UB_P1(2013, 512, 511, 6, 3)
+        UB_P1R(2014, 512, 511, 4, 2, ws.run_starts)
+        UB_P1R(2015, 512, 511, 4, 2, ws.run_rows + 32)
+        UB_P1R(2016, 512, 511, 4, 2, ws.run_rows + 1024)
 #undef UB_P1
+#undef UB_P1R
         // pass 2 over the 2048-key tiles the TB = 256 variants write (run_rows, columns)
 #define UB_H(G, D)                                                                                \
     case 2100 + 10 * G + D: {                                                                    \
@@ -305,8 +310,17 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
                 : launch_apply_g<kApplyStack, G, (int)kPartTileKeys>(ws, mmax, nullptr, 0, 0,     \
                                                                     res, st, s);                  \
         break;
-        UB_SG(4) UB_SG(8) UB_SG(16)
+        UB_SG(2) UB_SG(4) UB_SG(8) UB_SG(16)
 #undef UB_SG
+#define UB_SGD(G, D)                                                                              \
+    case 1000 + 10 * G + D:                                                                      \
+        e = big ? launch_apply_g<kApplyStack, G, 2 * (int)kPartTileKeys, D>(ws, mmax, nullptr, 0,  \
+                                                                           0, res, st, s)        \
+                : launch_apply_g<kApplyStack, G, (int)kPartTileKeys, D>(ws, mmax, nullptr, 0, 0,   \
+                                                                       res, st, s);              \
+        break;
+        UB_SGD(2, 1) UB_SGD(2, 4) UB_SGD(4, 1) UB_SGD(4, 4) UB_SGD(1, 2)
+#undef UB_SGD
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

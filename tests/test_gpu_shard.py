@@ -63,3 +63,48 @@ def test_sharded_probe_slices_concatenate(coracle):
             lo, hi = shard.probe_slice(gets.size, r, world)
             rows.append(bh.test_batch([f.clone()], gets[lo:hi].copy())[0])
         assert np.array_equal(np.concatenate(rows), want), world
+
+
+# ---- two or more GPUs in one process (skipped on a one-GPU box; the
+# driver's 8-GPU node runs them): the cross-device paths of SURVEY §8e.
+multi_gpu = pytest.mark.skipif(bh.device_count() < 2, reason="needs >= 2 GPUs")
+
+
+@multi_gpu
+@pytest.mark.parametrize("m", [655_360, 167_772_160])
+def test_clone_across_devices_peer_copy(coracle, m):
+    """bloomhip_clone to another GPU: hipMemcpyPeer over xGMI; the replica
+    probes on its own device with the source's answers."""
+    keys = np.sort(rand_keys(300_000, m % 89))
+    f = bh.BloomFilter(m, device=0)
+    f.set_batch_run(keys)
+    want = coracle.build(m, keys)
+    probe = rand_keys(200_003, 7)
+    probe[:100_000] = keys[:100_000]
+    ref = bh.test_batch([f], probe)[0]
+    for dev in range(1, bh.device_count()):
+        c = f.clone(device=dev)
+        assert c.device == dev
+        assert (c.words() == want).all(), dev
+        fa, ma = f.run_meta()
+        fb, mb = c.run_meta()
+        assert np.array_equal(fa, fb) and ma == mb
+        assert (bh.test_batch([c], probe)[0] == ref).all(), dev
+
+
+@multi_gpu
+def test_per_run_builds_on_two_devices_match_pins(golden):
+    """configs[4]'s sharding rule in one process: run r of the C5 fan-in on
+    device r % G (bloomhip/shard.py), every bitmap equal to its pinned digest
+    (two runs per device keeps it short)."""
+    import hashlib
+    from bloomhip import shard
+    from bloomhip import workloads as W
+    G = min(2, bh.device_count())
+    for r in range(2 * G):
+        dev = shard.rank_for_run(r, G)  # one device standing for each rank
+        assert dev == r % G
+        keys, m = W.c5_run(r)
+        f = bh.BloomFilter(m, device=dev)
+        f.set_batch(keys)
+        assert hashlib.sha256(f.words().tobytes()).hexdigest() == golden["oracle"]["c5"][r]["sha256"], r
