@@ -486,7 +486,8 @@ inline int apply_lanes_per_tile(size_t nbins, size_t tile_pos = kPartTilePos) {
 // whose run outlasts the first step is finished by a wave-uniform loop.
 constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2;
 
-template <int MODE, int G, int TILE_KEYS, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth>
+template <int MODE, int G, int TILE_KEYS, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth,
+          int WALK = 0>
 __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const uint64_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, uint32_t seg_bits, uint64_t m, uint32_t *__restrict__ words, uint64_t nw32,
@@ -628,6 +629,43 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         }
     };
 
+    if constexpr (WALK == 1) {
+        // Independent lane groups: group q (G lanes) walks tiles q, q + Q,
+        // q + 2Q, ... one step (G vectors) per iteration, moving to its next
+        // tile as soon as its run ends, so no group waits for the longest run
+        // of a batch.  The next step's vector is loaded before the current
+        // one is applied, and the next tile's run bounds one tile ahead.
+        constexpr int kGroupsPerWave = 64 / G;
+        const int Q = kGroupsPerWave * (BLOCK / 64);
+        auto bnd = [&](int tt) -> uint2 {
+            return tt < ntiles ? make_uint2(run_starts[(size_t)b * ntiles + tt],
+                                            run_starts[(size_t)(b + 1) * ntiles + tt])
+                               : make_uint2(0, 0);
+        };
+        int t = wave * kGroupsPerWave + tl;
+        uint2 r = bnd(t), rn = bnd(t + Q);
+        uint32_t vb = r.x / 6u;  // the group's step base (vector index)
+        // state after this step: advance within the run or to the next tile
+        auto step = [&](int &tt, uint2 &rr, uint2 &rrn, uint32_t &vvb) {
+            vvb += G;
+            if (6 * vvb >= rr.y) {
+                tt += Q;
+                rr = rrn;
+                vvb = rr.x / 6u;
+                rrn = bnd(tt + Q);
+            }
+        };
+        uint4 v = load(min(t, ntiles - 1), vb + sub);
+        while (__ballot(t < ntiles) != 0) {
+            int t2 = t;
+            uint2 r2 = r, rn2 = rn;
+            uint32_t vb2 = vb;
+            step(t2, r2, rn2, vb2);
+            const uint4 v2 = load(min(t2, ntiles - 1), vb2 + sub);
+            if (t < ntiles && 6 * vb < r.y) apply6(v, t, vb + sub, r);
+            t = t2; r = r2; rn = rn2; vb = vb2; v = v2;
+        }
+    } else {
     uint2 r[DEPTH];
     if (wave < nbatch) bounds(wave, r);
     for (int j = wave; j < nbatch; j += (BLOCK / 64)) {
@@ -652,6 +690,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         }
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) r[d] = rn[d];
+    }
     }
     if constexpr (PROBE) return;
     __syncthreads();
@@ -1354,12 +1393,13 @@ hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const Partiti
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
-template <int MODE, int G, int TK, int DEPTH = kApplyDepth>
+template <int MODE, int G, int TK, int DEPTH = kApplyDepth, int WALK = 0>
 hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                           uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                           hipStream_t stream) {
     static const bool attr_set = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_part_apply<MODE, G, TK, kApplyBlock, DEPTH>),
+        (void)hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kStackMaxBits / 8));
         return true;
@@ -1367,7 +1407,7 @@ hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *wo
     (void)attr_set;
     const size_t lds = (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
     if (lds > kStackMaxBits / 8) return hipErrorInvalidValue;
-    k_part_apply<MODE, G, TK, kApplyBlock, DEPTH><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
+    k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
         res, st);
     return hipGetLastError();
@@ -1378,7 +1418,11 @@ hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *w
                            uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                            hipStream_t stream) {
     switch (apply_lanes_per_tile(ws.nbins, 3 * TK)) {
-        case 4: return launch_apply_g<MODE, 4, TK>(ws, m, words, nw32, merge, res, st, stream);
+        case 4:  // builds: independent lane groups (C2 pass 2 39.5 -> 34.4 us, C4 1.39 -> 1.36 ms)
+            if constexpr (MODE == kApplyBuild)
+                return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
+            else
+                return launch_apply_g<MODE, 4, TK>(ws, m, words, nw32, merge, res, st, stream);
         case 8: return launch_apply_g<MODE, 8, TK>(ws, m, words, nw32, merge, res, st, stream);
         case 16: return launch_apply_g<MODE, 16, TK>(ws, m, words, nw32, merge, res, st, stream);
         default: return launch_apply_g<MODE, 32, TK>(ws, m, words, nw32, merge, res, st, stream);

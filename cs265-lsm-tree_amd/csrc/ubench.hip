@@ -177,8 +177,11 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     const ModParams mp = make_mod_params(m);
     PartitionWorkspace ws{};
     if (!plan_segments(m, device_cu_count(), &ws)) return -34;
-    const bool half = (variant >= 2004 && variant < 2200 && variant < 2011) || (variant >= 2100 && variant < 2200);  // 2048-key tiles (TB = 256)
-    ws.tile_keys = half ? kPartTileKeys / 2 : choose_tile_keys(ws.nbins);
+    // forced tile sizes for the shape sweeps: 2048 keys (TB = 256 pass 1 and
+    // the 21xx pass-2 variants), 4096 keys (202x pass 1, 22xx pass 2)
+    const bool half = (variant >= 2004 && variant <= 2010) || (variant >= 2100 && variant < 2200);
+    const bool t4k = (variant >= 2020 && variant < 2100) || (variant >= 2200 && variant < 2300);
+    ws.tile_keys = half ? kPartTileKeys / 2 : t4k ? kPartTileKeys : choose_tile_keys(ws.nbins);
     ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
     ws.pos = pos;
     ws.run_rows = runs;
@@ -208,6 +211,15 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
         UB_GD(1, 1) UB_GD(1, 2) UB_GD(1, 4) UB_GD(2, 1) UB_GD(2, 2) UB_GD(2, 4)
         UB_GD(4, 1) UB_GD(4, 2) UB_GD(4, 4)
 #undef UB_GD
+#define UB_IG(G)                                                                                  \
+    case 3000 + G:                                                                               \
+        e = big ? launch_apply_g<kApplyBuild, G, 2 * (int)kPartTileKeys, 1, 1>(ws, m, words, nw32, \
+                                                                          0, nullptr, StackTable{}, s) \
+                : launch_apply_g<kApplyBuild, G, (int)kPartTileKeys, 1, 1>(ws, m, words, nw32, 0,  \
+                                                                      nullptr, StackTable{}, s); \
+        break;
+        UB_IG(1) UB_IG(2) UB_IG(4) UB_IG(8)
+#undef UB_IG
         // pass-1 shapes: TB threads x 8 keys, histogram capacity MAXB, MINW
         // waves per SIMD (register cap), NWG workgroups per CU
 #define UB_P1(V, TB, MAXB, MINW, NWG) UB_P1R(V, TB, MAXB, MINW, NWG, ws.run_rows)
@@ -227,6 +239,7 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
         UB_P1(2007, 256, 511, 5, 5) UB_P1(2008, 256, 511, 6, 6)
         UB_P1(2011, 512, 511, 4, 2) UB_P1(2012, 512, 511, 5, 3) UB_P1(2013, 512, 511, 6, 3)
         UB_P1R(2014, 512, 511, 4, 2, ws.run_starts)
+        UB_P1(2021, 512, 1023, 4, 2) UB_P1(2022, 512, 4096, 4, 2)
         UB_P1R(2015, 512, 511, 4, 2, ws.run_rows + 32)
         UB_P1R(2016, 512, 511, 4, 2, ws.run_rows + 1024)
 #undef UB_P1
@@ -242,6 +255,19 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     }
         UB_H(2, 2) UB_H(4, 1) UB_H(4, 2) UB_H(4, 4) UB_H(8, 2)
 #undef UB_H
+        // pass 2 over tables the 20xx / 202x pass-1 variants wrote (run_rows, columns)
+#define UB_HW(V, TK, G, D, W)                                                                     \
+    case V: {                                                                                    \
+        PartitionWorkspace w2 = ws;                                                              \
+        w2.run_starts = ws.run_rows;                                                             \
+        e = launch_apply_g<kApplyBuild, G, TK, D, W>(w2, m, words, nw32, 0, nullptr,              \
+                                                     StackTable{}, s);                           \
+        break;                                                                                   \
+    }
+        UB_HW(2191, 2048, 1, 1, 1) UB_HW(2192, 2048, 2, 1, 1) UB_HW(2194, 2048, 4, 1, 1)
+        UB_HW(2242, 4096, 4, 2, 0) UB_HW(2282, 4096, 8, 2, 0) UB_HW(2291, 4096, 1, 1, 1)
+        UB_HW(2292, 4096, 2, 1, 1) UB_HW(2294, 4096, 4, 1, 1)
+#undef UB_HW
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;
@@ -321,6 +347,15 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
         break;
         UB_SGD(2, 1) UB_SGD(2, 4) UB_SGD(4, 1) UB_SGD(4, 4) UB_SGD(1, 2)
 #undef UB_SGD
+#define UB_SIG(G)                                                                                 \
+    case 3000 + G:                                                                               \
+        e = big ? launch_apply_g<kApplyStack, G, 2 * (int)kPartTileKeys, 1, 1>(ws, mmax, nullptr,  \
+                                                                          0, 0, res, st, s)      \
+                : launch_apply_g<kApplyStack, G, (int)kPartTileKeys, 1, 1>(ws, mmax, nullptr, 0,   \
+                                                                      0, res, st, s);            \
+        break;
+        UB_SIG(1) UB_SIG(2) UB_SIG(4) UB_SIG(8)
+#undef UB_SIG
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

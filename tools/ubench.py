@@ -77,18 +77,27 @@ def part_phases(n=16_777_216, bpe=10.0, reps=50):
                              words.data_ptr(), s.cuda_stream)
         assert rc == 0, (v, rc)
     names = {0: "pass 1", 1: "pass 2 (product G)", 4: "pass 2 G=4",
-             8: "pass 2 G=8", 16: "pass 2 G=16", 32: "pass 2 G=32"}
+             8: "pass 2 G=8", 16: "pass 2 G=16", 32: "pass 2 G=32",
+             3001: "pass 2 indep groups G=1", 3002: "pass 2 indep G=2", 3004: "pass 2 indep G=4",
+             3008: "pass 2 indep G=8"}
     if os.environ.get("UB_P1"):
+        # order matters: the 21xx pass-2 variants read the table the last
+        # 2048-key-tile pass 1 (2007) wrote
         names = {0: "pass 1", 2001: "pass 1 TB512 maxb1024 4w", 2002: "pass 1 TB512 maxb1024 5w 3wg",
-                 2003: "pass 1 TB512 maxb1024 6w 3wg", 2004: "pass 1 TB256 5w 5wg",
-                 2005: "pass 1 TB256 6w 5wg", 2006: "pass 1 TB256 4w 4wg",
-                 2007: "pass 1 TB256 maxb511 5w 5wg", 2008: "pass 1 TB256 maxb511 6w 6wg",
-                 2011: "pass 1 TB512 maxb511 4w", 2012: "pass 1 TB512 maxb511 5w 3wg",
-                 2013: "pass 1 TB512 maxb511 6w 3wg", 2014: "pass 1 = 2011, table at run_starts",
-                 2015: "pass 1 = 2011, table at rows+128B", 2016: "pass 1 = 2011, table at rows+4KB",
-                 2122: "pass 2 (2048-key tiles) G=2 d=2", 2141: "pass 2 (2048) G=4 d=1",
-                 2142: "pass 2 (2048) G=4 d=2", 2144: "pass 2 (2048) G=4 d=4",
-                 2182: "pass 2 (2048) G=8 d=2"}
+                 2003: "pass 1 TB512 maxb1024 6w 3wg", 2011: "pass 1 TB512 maxb511 4w",
+                 2013: "pass 1 TB512 maxb511 6w 3wg",
+                 2004: "pass 1 TB256 5w 5wg", 2006: "pass 1 TB256 4w 4wg",
+                 2008: "pass 1 TB256 maxb511 6w 6wg", 2007: "pass 1 TB256 maxb511 5w 5wg",
+                 2122: "pass 2 (2048-key tiles) G=2 d=2", 2142: "pass 2 (2048) G=4 d=2",
+                 2192: "pass 2 (2048) indep G=2", 2194: "pass 2 (2048) indep G=4",
+                 2191: "pass 2 (2048) indep G=1"}
+    if os.environ.get("UB_T4K"):  # C5 etc. on 4096-key tiles (TB = 512 pass 1)
+        names = {0: "pass 1 (product)", 1: "pass 2 (product)", 3002: "pass 2 indep G=2",
+                 3004: "pass 2 indep G=4",
+                 2021: "pass 1 TB512 4096-key tiles maxb1023", 2242: "pass 2 (4096) G=4 d=2",
+                 2282: "pass 2 (4096) G=8 d=2", 2291: "pass 2 (4096) indep G=1",
+                 2292: "pass 2 (4096) indep G=2", 2294: "pass 2 (4096) indep G=4",
+                 2022: "pass 1 TB512 4096-key tiles maxb4096"}
     if os.environ.get("UB_GD"):
         names = {0: "pass 1", 1: "pass 2 (product G)"}
         names.update({1000 + 10 * g + d: f"pass 2 G={g} depth={d}"
@@ -105,9 +114,24 @@ def part_phases(n=16_777_216, bpe=10.0, reps=50):
     if os.environ.get("UB_P1"):
         run(0); run(1)
         ref = words.clone()
-        words.zero_(); run(2006); run(2142)
+        for p2 in (2142, 2192, 2194):
+            words.zero_(); run(2007); run(p2)
+            torch.cuda.synchronize()
+            print(json.dumps({"check": f"2048-key tiles {p2} bitmap == product", "ok": bool(torch.equal(ref, words))}))
+    if os.environ.get("UB_T4K"):
+        run(0); run(1)
+        ref = words.clone()
+        p1 = 2021 if nbins <= 1023 else 2022
+        for p2 in (2242, 2294):
+            words.zero_(); run(p1); run(p2)
+            torch.cuda.synchronize()
+            print(json.dumps({"check": f"4096-key tiles {p2} bitmap == product", "ok": bool(torch.equal(ref, words))}))
+    run(0); run(1)
+    ref = words.clone()
+    for v in (3001, 3002, 3004, 3008):
+        words.zero_(); run(v)
         torch.cuda.synchronize()
-        print(json.dumps({"check": "2048-key tiles bitmap == product", "ok": bool(torch.equal(ref, words))}))
+        print(json.dumps({"check": f"indep walk {v} bitmap == product", "ok": bool(torch.equal(ref, words))}), flush=True)
     names = dict(names)
     names[-1] = "pass 1 (again, last)"
     if os.environ.get("UB_ALT"):
@@ -159,10 +183,19 @@ def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
                                 runs.data_ptr(), res.data_ptr(), slots.data_ptr(), out.data_ptr(),
                                 s.cuda_stream)
     assert run(0) == 0
+    torch.cuda.synchronize()
+    ref = out.clone()
+    for v in (3001, 3002, 3004, 3008):
+        out.zero_()
+        assert run(1) == 0 and run(v) == 0 and run(5) == 0
+        torch.cuda.synchronize()
+        print(json.dumps({"check": f"stack indep walk {v} == product", "ok": bool(torch.equal(ref, out))}), flush=True)
     names = {0: "all three", 1: "pass 1 (+slots, +transpose)", 2: "pass 2", 5: "combine",
              102: "pass 2 G=2", 104: "pass 2 G=4", 108: "pass 2 G=8", 116: "pass 2 G=16",
              1021: "pass 2 G=2 d=1", 1024: "pass 2 G=2 d=4", 1041: "pass 2 G=4 d=1",
-             1044: "pass 2 G=4 d=4", 1012: "pass 2 G=1 d=2"}
+             1044: "pass 2 G=4 d=4", 1012: "pass 2 G=1 d=2",
+             3001: "pass 2 indep G=1", 3002: "pass 2 indep G=2", 3004: "pass 2 indep G=4",
+             3008: "pass 2 indep G=8"}
     for v in names:
         if run(v) != 0:
             continue
