@@ -487,7 +487,7 @@ inline int apply_lanes_per_tile(size_t nbins, size_t tile_pos = kPartTilePos) {
 constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2;
 
 template <int MODE, int G, int TILE_KEYS, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth,
-          int WALK = 0>
+          int WALK = 0, int NF = 0>
 __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const uint64_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, uint32_t seg_bits, uint64_t m, uint32_t *__restrict__ words, uint64_t nw32,
@@ -517,7 +517,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         // Word-interleaved image: member j's word p at seg[p * nf + j], so an
         // entry's nf words sit together and one address (+ immediate offsets)
         // reaches all of them.
-        const int nf = st.nf;
+        const int nf = NF ? NF : st.nf;  // NF: the member count as a compile-time constant
         for (int j = 0; j < nf; j++) {
             const uint32_t mw = st.mwords[j];
             const uint32_t start = (uint32_t)(((uint64_t)b * seg_words) % mw);
@@ -600,12 +600,18 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                 mask |= ok << k;
                 const uint32_t o = ok ? (e[k] - base21) & kEntryMask : 0u;  // reads stay in the image
                 if constexpr (MODE == kApplyStack) {
-                    const uint32_t *wp = seg + __umul24(o >> 5, (uint32_t)st.nf);
                     const uint32_t sh = o & 31;
                     uint32_t acc = 0;
+                    if constexpr (NF > 0) {  // straight-line: NF reads at immediate offsets
+                        const uint32_t *wp = seg + (o >> 5) * (uint32_t)NF;
 #pragma unroll
-                    for (int j = 0; j < kMaxStack; j++)  // member j's word at immediate offset 4j
-                        if (j < st.nf) acc |= __builtin_amdgcn_ubfe(wp[j], sh, 1u) << j;
+                        for (int j = 0; j < NF; j++) acc |= __builtin_amdgcn_ubfe(wp[j], sh, 1u) << j;
+                    } else {
+                        const uint32_t *wp = seg + __umul24(o >> 5, (uint32_t)st.nf);
+#pragma unroll
+                        for (int j = 0; j < kMaxStack; j++)  // member j's word at immediate offset 4j
+                            if (j < st.nf) acc |= __builtin_amdgcn_ubfe(wp[j], sh, 1u) << j;
+                    }
                     bits[k] = acc;
                 } else {
                     bits[k] = (seg[o >> 5] >> (o & 31)) & 1u;
@@ -1393,13 +1399,14 @@ hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const Partiti
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
-template <int MODE, int G, int TK, int DEPTH = kApplyDepth, int WALK = 0>
+template <int MODE, int G, int TK, int DEPTH = kApplyDepth, int WALK = 0, int NF = 0>
 hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                           uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                           hipStream_t stream) {
+    if (NF && st.nf != NF) return hipErrorInvalidValue;
     static const bool attr_set = [] {
         (void)hipFuncSetAttribute(
-            reinterpret_cast<const void *>(&k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK>),
+            reinterpret_cast<const void *>(&k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK, NF>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kStackMaxBits / 8));
         return true;
@@ -1407,16 +1414,35 @@ hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *wo
     (void)attr_set;
     const size_t lds = (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
     if (lds > kStackMaxBits / 8) return hipErrorInvalidValue;
-    k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
+    k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK, NF><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
         res, st);
     return hipGetLastError();
+}
+
+// The stacked pass 2 with the member count compiled in (straight-line member
+// reads instead of a guarded loop over up to kMaxStack), G lanes per tile.
+template <int G, int TK, int WALK = 0>
+hipError_t launch_stack_nf(const PartitionWorkspace &ws, uint64_t m, uint8_t *res,
+                           const StackTable &st, hipStream_t stream) {
+    switch (st.nf) {
+#define STACK_NF(N) \
+    case N: return launch_apply_g<kApplyStack, G, TK, kApplyDepth, WALK, N>(ws, m, nullptr, 0, 0, res, st, stream);
+        STACK_NF(2) STACK_NF(3) STACK_NF(4) STACK_NF(5) STACK_NF(6) STACK_NF(7) STACK_NF(8)
+#undef STACK_NF
+        default: return launch_apply_g<kApplyStack, G, TK, kApplyDepth, WALK>(ws, m, nullptr, 0, 0, res, st, stream);
+    }
 }
 
 template <int MODE, int TK>
 hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                            uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                            hipStream_t stream) {
+    if constexpr (MODE == kApplyStack) {
+        if (apply_lanes_per_tile(ws.nbins, 3 * TK) <= 4)
+            return launch_stack_nf<4, TK>(ws, m, res, st, stream);
+        return launch_stack_nf<8, TK>(ws, m, res, st, stream);
+    }
     switch (apply_lanes_per_tile(ws.nbins, 3 * TK)) {
         case 4:  // builds: independent lane groups (C2 pass 2 39.5 -> 34.4 us, C4 1.39 -> 1.36 ms)
             if constexpr (MODE == kApplyBuild)

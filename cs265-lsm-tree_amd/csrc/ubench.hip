@@ -356,6 +356,23 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
         break;
         UB_SIG(1) UB_SIG(2) UB_SIG(4) UB_SIG(8)
 #undef UB_SIG
+        // the runtime-nf kernel (the product compiles nf in): A/B of the straight-line reads
+        case 3952:
+            e = big ? launch_stack_nf<2, 2 * (int)kPartTileKeys, 1>(ws, mmax, res, st, s)
+                    : launch_stack_nf<2, (int)kPartTileKeys, 1>(ws, mmax, res, st, s);
+            break;
+        case 3954:
+            e = big ? launch_stack_nf<4, 2 * (int)kPartTileKeys, 1>(ws, mmax, res, st, s)
+                    : launch_stack_nf<4, (int)kPartTileKeys, 1>(ws, mmax, res, st, s);
+            break;
+        case 3958:
+            e = big ? launch_stack_nf<8, 2 * (int)kPartTileKeys, 0>(ws, mmax, res, st, s)
+                    : launch_stack_nf<8, (int)kPartTileKeys, 0>(ws, mmax, res, st, s);
+            break;
+        case 3900:
+            e = big ? launch_apply_g<kApplyStack, 4, 2 * (int)kPartTileKeys>(ws, mmax, nullptr, 0, 0, res, st, s)
+                    : launch_apply_g<kApplyStack, 4, (int)kPartTileKeys>(ws, mmax, nullptr, 0, 0, res, st, s);
+            break;
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

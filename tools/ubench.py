@@ -185,7 +185,7 @@ def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
     assert run(0) == 0
     torch.cuda.synchronize()
     ref = out.clone()
-    for v in (3001, 3002, 3004, 3008):
+    for v in (3001, 3002, 3004, 3008, 3900, 3952, 3954, 3958):
         out.zero_()
         assert run(1) == 0 and run(v) == 0 and run(5) == 0
         torch.cuda.synchronize()
@@ -195,15 +195,18 @@ def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
              1021: "pass 2 G=2 d=1", 1024: "pass 2 G=2 d=4", 1041: "pass 2 G=4 d=1",
              1044: "pass 2 G=4 d=4", 1012: "pass 2 G=1 d=2",
              3001: "pass 2 indep G=1", 3002: "pass 2 indep G=2", 3004: "pass 2 indep G=4",
-             3008: "pass 2 indep G=8"}
+             3008: "pass 2 indep G=8", 3900: "pass 2 runtime nf G=4 (old product)", -2: "pass 2 again",
+             3952: "pass 2 nf const indep G=2", 3954: "pass 2 nf const indep G=4",
+             3958: "pass 2 nf const batch G=8", -3954: "nf const indep G=4 again"}
     for v in names:
-        if run(v) != 0:
+        vv = abs(v)
+        if run(vv) != 0:
             continue
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
         for _ in range(20):
-            run(v)
+            run(vv)
         b.record(s)
         torch.cuda.synchronize()
         print(json.dumps({"op": "stacked probe", "levels": list(levels_sel), "nbins": nb.value,
