@@ -89,10 +89,12 @@ def cpu_baseline(keys, m, reps=5):
     T = os.cpu_count() or 1
     C.build_mt(m, keys[:1_000_000], T)  # warm-up (threads, pages)
     t = _med(lambda: C.build_mt(m, keys, T), reps)
+    quota = host_cpu_info().get("cgroup_cpu_quota")
     return {"value": round(keys.size / t / 1e9, 5), "unit": "Gkeys/s", "cores": T,
             "kind": "port",
             "sample": f"full C2 run: {keys.size} keys, m={m}; oracle/bloom_oracle.c -O2 on "
-                      f"{T} native threads (nproc), median of {reps} ({t * 1e3:.1f} ms each)"}
+                      f"{T} native threads (nproc), median of {reps} ({t * 1e3:.1f} ms each)"
+                      + (f"; this process's cgroup CPU quota is {quota} CPUs" if quota else "")}
 
 
 def cpu_baseline_detail(keys, m):
@@ -695,6 +697,13 @@ def main():
                      "note": "achieved = (4N + m/8) per build / device time per build, HIP "
                              "events on the launch stream around the unprofiled timed loop; "
                              "profiled_kernel_ms = per-launch events in a separate pass"},
+        # The build's real ceiling is the VALU: the reference's three 64-bit hashes and
+        # exact remainders alone run at 410-420 Gkeys/s on this chip (tools/ubench.py,
+        # compute only), i.e. 2.2 TB/s = 0.27 of HBM at 5.25 B/key.
+        "compute_ceiling": {"bound": "valu", "unit": "Gkeys/s", "hash_mod_only": 410.0,
+                            "achieved": round(n / (dev_ms_per_step * 1e-3) / 1e9, 2),
+                            "frac": round(n / (dev_ms_per_step * 1e-3) / 1e9 / 410.0, 4),
+                            "source": "profiles/r01/ubench_primitives.jsonl (hash3+mod_fast)"},
         "clocks": clocks,
         "cpu_baseline": cpu,
         "kernels": kernels,
