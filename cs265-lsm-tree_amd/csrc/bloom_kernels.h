@@ -68,7 +68,7 @@ constexpr size_t kPartTileKeys = (size_t)kPartBlock * kPartKPT;  // 4096
 constexpr int kPartTilePos = (int)kPartTileKeys * 3;
 constexpr size_t kPartMaxBins = 4096;     // segments of a 4096-key tile (512 threads)
 constexpr size_t kPartMaxBinsBig = 8192;  // segments of an 8192-key tile (1024 threads)
-constexpr size_t kPartMaxSub = 8192;      // p >> sub_shift below this (SegMap's domain)
+constexpr size_t kPartMaxSub = 16384;     // p >> sub_shift below this (SegMap's domain)
 
 // Sorted-tile entries: the low kEntryBits bits of each position, three per
 // u64 (bits 0-20, 21-41, 42-62).  A segment has at most kStackMaxBits <
@@ -131,7 +131,8 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
 // CUs of the current device (cached).
 int device_cu_count();
 // Fills the geometry fields of ws for a filter of m bits; false when the
-// partition path does not apply (m > kPartMaxSub * 2^20 = 2^33 bits).
+// partition path does not apply (more than kPartMaxBinsBig segments of at
+// most 160 KiB: m above about 2^33.3 bits).
 bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws);
 
 // Probe: filters up to this size are gathered directly; larger ones use the

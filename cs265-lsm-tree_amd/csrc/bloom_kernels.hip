@@ -1236,7 +1236,7 @@ bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
     uint64_t nsub = ((m - 1) >> s) + 1;
     uint64_t g = (nsub + W - 1) / W;
     while (g > 1 && (g << s) > seg_max) g--;
-    if ((g << s) > seg_max) return false;  // m > kPartMaxSub * 2^20
+    if ((g << s) > seg_max) return false;  // m > kPartMaxSub * 2^20 (nbins caps it lower)
     // 128-B aligned segments for the 16-B segment stores.
     while (((g << s) % 1024) != 0) g++;
     if ((g << s) > seg_max) return false;

@@ -1,4 +1,3 @@
 set -o pipefail
-D=gpurun_out/xp23; mkdir -p $D
-export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/stats_c3 -o run --output-format csv -- python tools/probe_prof.py auto 30 > $D/stats_c3.log 2>&1 || exit 1
+D=gpurun_out/xp26; mkdir -p $D
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/pytest.log 2>&1 || exit 1
