@@ -176,7 +176,9 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
     const ModParams mp = make_mod_params(m);
     PartitionWorkspace ws{};
-    if (!plan_segments(m, device_cu_count(), &ws)) return -34;
+    // 40xx: segments planned for twice the CU count (two pass-2 workgroups per CU)
+    if (!plan_segments(m, (variant >= 4000 && variant < 4100 ? 2 : 1) * device_cu_count(), &ws))
+        return -34;
     // forced tile sizes for the shape sweeps: 2048 keys (TB = 256 pass 1 and
     // the 21xx pass-2 variants), 4096 keys (202x pass 1, 22xx pass 2)
     const bool half = (variant >= 2004 && variant <= 2010) || (variant >= 2100 && variant < 2200);
@@ -190,8 +192,8 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     hipError_t e = hipSuccess;
     const bool big = ws.tile_keys == 2 * kPartTileKeys;
     switch (variant) {
-        case 0: e = launch_part_bin(ks, mp, ws, s); break;
-        case 1: e = launch_part_apply(mp, words, ws, 0, s); break;
+        case 0: case 4000: e = launch_part_bin(ks, mp, ws, s); break;
+        case 1: case 4001: e = launch_part_apply(mp, words, ws, 0, s); break;
 #define UB_G(G)                                                                                   \
     case G:                                                                                       \
         e = big ? launch_apply_g<kApplyBuild, G, 2 * (int)kPartTileKeys>(ws, m, words, nw32, 0,   \

@@ -68,7 +68,7 @@ def part_phases(n=16_777_216, bpe=10.0, reps=50):
     assert LIB.ubench_part_geometry(n, m, geo.ctypes.data) == 0
     nbins, seg_bits, tk, ntiles = (int(x) for x in geo)
     pos = torch.empty(ntiles * tk, dtype=torch.int64, device="cuda")
-    runs = torch.empty(ntiles * (nbins + 1) * 2, dtype=torch.int32, device="cuda")
+    runs = torch.empty(ntiles * (nbins + 1) * 4, dtype=torch.int32, device="cuda")  # room for the 2x-segment plans
     words = torch.zeros((m + 63) // 64 * 2, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
 
@@ -134,13 +134,21 @@ def part_phases(n=16_777_216, bpe=10.0, reps=50):
         print(json.dumps({"check": f"indep walk {v} bitmap == product", "ok": bool(torch.equal(ref, words))}), flush=True)
     if os.environ.get("UB_QUICK"):
         names = {0: "pass 1", 1: "pass 2 (product)"}
+    if os.environ.get("UB_2X"):  # segments for twice the CU count (two pass-2 WGs per CU)
+        run(4000); run(4001)
+        w2 = words.clone()
+        run(0); run(1)
+        print(json.dumps({"check": "2x-segment plan bitmap == product", "ok": bool(torch.equal(w2, words))}), flush=True)
+        names = {0: "pass 1", 1: "pass 2 (product)", 4000: "pass 1 (2x segments)",
+                 4001: "pass 2 (2x segments)", -4000: "pass 1 (2x) again", -5: "pass 2 again",
+                 -4001: "pass 2 (2x) again"}
     names = dict(names)
     names[-1] = "pass 1 (again, last)"
     if os.environ.get("UB_ALT"):
         names = {0: "pass 1 product", 2014: "2011 at run_starts", -1: "product", -2014: "2011 again",
                  -2: "product", -3: "2011 again"}
     for v, name in names.items():
-        ms = _events(lambda: run({-1: 0, -2: 0, -3: 2014}.get(v, abs(v))), reps)
+        ms = _events(lambda: run({-1: 0, -2: 0, -3: 2014, -5: 1}.get(v, abs(v))), reps)
         print(json.dumps({"op": "partition build", "n": n, "m": m, "nbins": nbins,
                           "seg_bits": seg_bits, "tile_keys": tk, "phase": name,
                           "us": round(ms * 1e3, 1)}), flush=True)
