@@ -60,22 +60,55 @@ BH_HD uint64_t raw_hash1(int32_t k) {  // src/bloom_filter.cpp:8-20
     return x;
 }
 
+// (x ^ c) ^ (x >> S) for a 32-bit constant c: on gfx950 one 64-bit shift, one
+// xor of the high words and one three-input xor of the low words (gfx950
+// v_bitop3_b32 with truth table 0x96 = a ^ b ^ c; the compiler
+// splits the shift into an alignbit + a second shift and xors c separately:
+// 4 instructions against 3).
+template <int S>
+BH_HD uint64_t xor_shr_c(uint64_t x, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint64_t t;
+    asm("v_lshrrev_b64 %0, %2, %1" : "=v"(t) : "v"(x), "i"(S));
+    uint32_t lo;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(lo) : "v"((uint32_t)x), "v"((uint32_t)t), "s"(c));
+    const uint32_t hi = (uint32_t)(x >> 32) ^ (uint32_t)(t >> 32);
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return (x ^ c) ^ (x >> S);
+#endif
+}
+
 BH_HD uint64_t raw_hash2(int32_t k) {  // src/bloom_filter.cpp:22-34
     uint64_t x = (uint64_t)((int64_t)k * 4097 + 0x7ed55d16);  // (x + 0x7ed55d16) + (x << 12)
-    x = (x ^ 0xc761c23cu) ^ (x >> 19);
+    x = xor_shr_c<19>(x, 0xc761c23cu);                          // (x ^ 0xc761c23c) ^ (x >> 19)
     x = (x + 0x165667b1u) + (x << 5);
     x = (x + 0xd3a2646cu) ^ (x << 9);
     x = (x + 0xfd7046c5u) + (x << 3);
-    x = (x ^ 0xb55a4f09u) ^ (x >> 16);
+    x = xor_shr_c<16>(x, 0xb55a4f09u);                          // (x ^ 0xb55a4f09) ^ (x >> 16)
     return x;
 }
 
 BH_HD uint64_t raw_hash3(int32_t k) {  // src/bloom_filter.cpp:36-47
+#if defined(__HIP_DEVICE_COMPILE__)
+    // (x ^ 61) ^ (x >> 16) on the sign-extended key, by halves: the high word
+    // of x is s = 0 or ~0 (the sign), so the result's high word is
+    // s ^ (s >> 16) = s & 0xFFFF0000 and its low word k ^ 61 ^ alignbit(s, k, 16)
+    // (one v_bitop3_b32 xor3; 61 is an inline constant).
+    const uint32_t xl = (uint32_t)k, xh = (uint32_t)(k >> 31);
+    uint32_t lo;
+    asm("v_bitop3_b32 %0, %1, %2, 61 bitop3:0x96" : "=v"(lo) : "v"(xl), "v"(__builtin_amdgcn_alignbit(xh, xl, 16)));
+    uint64_t x = ((uint64_t)(xh & 0xFFFF0000u) << 32) | lo;
+#else
     uint64_t x = (uint64_t)(int64_t)k;
     x = (x ^ 61u) ^ (x >> 16);
+#endif
     x = lshl_add64<3>(x, x);                            // x = x + (x << 3)
     x = x ^ (x >> 4);
-    x = x * 0x27d4eb2du;
+    // x * 0x27d4eb2d mod 2^64 as lo32 * c (one v_mad_u64_u32) plus hi32 * c in
+    // the high word (v_mul_lo_u32): the compiler's 64-bit multiply takes two
+    // v_mad_u64_u32 and two moves
+    x = (uint64_t)(uint32_t)x * 0x27d4eb2du + ((uint64_t)((uint32_t)(x >> 32) * 0x27d4eb2du) << 32);
     x = x ^ (x >> 15);
     return x;
 }

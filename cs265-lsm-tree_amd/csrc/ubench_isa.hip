@@ -47,6 +47,8 @@ DEF32(k_alignbit, "v_alignbit_b32 %0, %0, %1, 12")
 DEF32(k_mad_u32_u24, "v_mad_u32_u24 %0, %0, %1, %0")
 DEF32(k_add_u32, "v_add_u32 %0, %1, %0")
 DEF32(k_lshl_add_u32, "v_lshl_add_u32 %0, %0, 3, %0")
+DEF32(k_bitop3_xor3, "v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96")
+DEF32(k_alignbit16, "v_alignbit_b32 %0, %0, %0, 16")
 
 extern "C" int ubench_isa(int which, uint64_t *sink, int grid, int block, int iters, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -63,6 +65,8 @@ extern "C" int ubench_isa(int which, uint64_t *sink, int grid, int block, int it
         case 9: k_mad_u32_u24<<<grid, block, 0, s>>>(iters, sink); break;
         case 10: k_add_u32<<<grid, block, 0, s>>>(iters, sink); break;
         case 11: k_lshl_add_u32<<<grid, block, 0, s>>>(iters, sink); break;
+        case 12: k_bitop3_xor3<<<grid, block, 0, s>>>(iters, sink); break;
+        case 13: k_alignbit16<<<grid, block, 0, s>>>(iters, sink); break;
         default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -28,6 +28,7 @@ for s in ${STEPS//,/ }; do
     bench_quick) run bench_quick 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline || exit 1 ;;
     bench_c4) run bench_c4 400 python bench.py --workload c4 --steps 5 --warmup 1 --no-extras --no-cpu-baseline || exit 1 ;;
     bench_c4w) run bench_c4w 400 python bench.py --workload c4w --steps 5 --warmup 1 --no-extras --no-cpu-baseline || exit 1 ;;
+    ub_isa) run ub_isa 120 python tools/ubench_isa.py || exit 1 ;;
     ub_part) run ub_part 300 python tools/ubench.py part || exit 1 ;;
     ub_part_c5) run ub_part_c5 300 python tools/ubench.py part_c5 || exit 1 ;;
     ub_part_c4) run ub_part_c4 300 python tools/ubench.py part_c4 || exit 1 ;;
