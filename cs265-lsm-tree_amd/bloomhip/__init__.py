@@ -24,7 +24,9 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(os.path.dirname(PKG_DIR), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libbloomhip.so")
+# BLOOMHIP_LIB: another build of the same library (tools/ab.sh times two
+# builds of the engine against each other in one GPU session).
+LIB_PATH = os.environ.get("BLOOMHIP_LIB") or os.path.join(LIB_DIR, "libbloomhip.so")
 
 OK = 0
 EIO = -5

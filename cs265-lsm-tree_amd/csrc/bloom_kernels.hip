@@ -142,6 +142,20 @@ __global__ void __launch_bounds__(kBlock) k_build_lds(KeySpan ks, ModParams mp,
 // position got in the sorted tile: slots[(tile*3 + h)*tile_keys + key].
 // ---------------------------------------------------------------------------
 
+// Inclusive prefix sum across the 64 lanes of a wave in DPP steps (no LDS):
+// row_shr 1/2/4/8 inside each row of 16 lanes (a lane with no source keeps
+// the old value 0), then row_bcast:15 (row r's last lane into row r + 1,
+// rows 1 and 3) and row_bcast:31 (lane 31 into rows 2 and 3).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
 // Workgroup barrier that waits for this wave's LDS operations only.
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -301,31 +315,33 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
 
         // 2. exclusive scan of the nbins+1 counts (the extra slot is 0 and
         //    receives the tile total); thread t owns [t*per, t*per + per).
+        //    Waves that own no bin (C2: waves 5-7 of 8) skip it: nobody
+        //    reads their wave sums, which come after every live bin.
+        const bool scan_wave = wave * 64 * per <= nb;  // uniform per wave
         uint32_t local[kScanPer];  // 4 * count of bin b
-        uint32_t tsum = 0;
+        uint32_t tsum = 0, incl = 0;
+        if (scan_wave) {
 #pragma unroll
-        for (int q = 0; q < kScanPer; q++) {
-            const int b = tid * per + q;
-            local[q] = (q < per && b <= nb) ? s_hist[b] - ((uint32_t)b << kBinShift) : 0u;
-            tsum += local[q];
+            for (int q = 0; q < kScanPer; q++) {
+                const int b = tid * per + q;
+                local[q] = (q < per && b <= nb) ? s_hist[b] - ((uint32_t)b << kBinShift) : 0u;
+                tsum += local[q];
+            }
+            incl = wave_incl_scan(tsum);
+            if (lane == 63) s_wsum[wave] = incl;
         }
-        uint32_t incl = tsum;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += o;
-        }
-        if (lane == 63) s_wsum[wave] = incl;
         lds_barrier();
-        uint32_t run = incl - tsum;
-        for (int w = 0; w < wave; w++) run += s_wsum[w];
+        if (scan_wave) {
+            uint32_t run = incl - tsum;
+            for (int w = 0; w < wave; w++) run += s_wsum[w];
 #pragma unroll
-        for (int q = 0; q < kScanPer; q++) {
-            const int b = tid * per + q;
-            if (q < per && b <= nb) {
-                // biased by -(b << kBinShift): bin + rank value = byte slot
-                s_hist[b] = run - ((uint32_t)b << kBinShift);
-                run += local[q];
+            for (int q = 0; q < kScanPer; q++) {
+                const int b = tid * per + q;
+                if (q < per && b <= nb) {
+                    // biased by -(b << kBinShift): bin + rank value = byte slot
+                    s_hist[b] = run - ((uint32_t)b << kBinShift);
+                    run += local[q];
+                }
             }
         }
         lds_barrier();
