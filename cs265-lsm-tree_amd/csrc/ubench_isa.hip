@@ -71,3 +71,29 @@ extern "C" int ubench_isa(int which, uint64_t *sink, int grid, int block, int it
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+
+// Semantics probe: v_lshl_add_u64 with immediate shifts 0..7 on n inputs
+// (the CDNA3 ISA guide limits the shift to 0..4); out[8 * i + s].
+template <int S>
+__device__ uint64_t lshl_add_imm(uint64_t a, uint64_t b) {
+    uint64_t r;
+    asm volatile("v_lshl_add_u64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(S), "v"(b));
+    return r;
+}
+__global__ void k_lshl_add_check(const uint64_t *in, uint64_t *out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a = in[2 * i], b = in[2 * i + 1];
+    out[8 * i + 0] = lshl_add_imm<0>(a, b);
+    out[8 * i + 1] = lshl_add_imm<1>(a, b);
+    out[8 * i + 2] = lshl_add_imm<2>(a, b);
+    out[8 * i + 3] = lshl_add_imm<3>(a, b);
+    out[8 * i + 4] = lshl_add_imm<4>(a, b);
+    out[8 * i + 5] = lshl_add_imm<5>(a, b);
+    out[8 * i + 6] = lshl_add_imm<6>(a, b);
+    out[8 * i + 7] = lshl_add_imm<7>(a, b);
+}
+extern "C" int ubench_lshl_add_check(const uint64_t *in, uint64_t *out, int n, void *stream) {
+    k_lshl_add_check<<<(n + 255) / 256, 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(in, out, n);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}

@@ -43,5 +43,29 @@ def main():
                           "simd_cycles_per_wave_instr_at_2.4GHz": round(t * sclk / per_simd, 2)}))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("UB_CHECK"):
     main()
+
+
+def lshl_add_check(n=1 << 20):
+    """v_lshl_add_u64 with immediate shifts 0..7 against (a << s) + b."""
+    import numpy as np
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    ab = rng.integers(0, 2**63, size=2 * n, dtype=np.int64).view(np.uint64)
+    ab[:64] = np.uint64(2**64 - 1)
+    inp = torch.from_numpy(ab.view(np.int64)).to(dev)
+    out = torch.empty(8 * n, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    assert LIB.ubench_lshl_add_check(ctypes.c_void_p(inp.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                     n, ctypes.c_void_p(s.cuda_stream)) == 0
+    got = out.cpu().numpy().view(np.uint64).reshape(n, 8)
+    a, b = ab[0::2], ab[1::2]
+    for sh in range(8):
+        want = (a << np.uint64(sh)) + b
+        print(json.dumps({"v_lshl_add_u64_shift": sh, "exact": bool((got[:, sh] == want).all()),
+                          "mismatches": int((got[:, sh] != want).sum())}))
+
+
+if __name__ == "__main__" and os.environ.get("UB_CHECK"):
+    lshl_add_check()
