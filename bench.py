@@ -145,6 +145,13 @@ def kernel_source_sha():
     return h.hexdigest()[:16]
 
 
+def library_kernel_sha():
+    """The same digest as compiled into the loaded library (the kernels that
+    actually run); differs from kernel_source_sha() when lib/ is stale."""
+    import bloomhip as bh
+    return bh.lib().bloomhip_kernel_sha().decode()
+
+
 def pmc_traffic(workload):
     """HBM bytes per build from the committed rocprofv3 PMC summary
     (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md
@@ -154,7 +161,7 @@ def pmc_traffic(workload):
         return None
     with open(path) as f:
         d = json.load(f)
-    if d.get("kernel_source_sha") != kernel_source_sha():
+    if d.get("kernel_source_sha") != library_kernel_sha():
         return {"stale": True, "file": os.path.relpath(path, ROOT)}
     return d
 
@@ -698,13 +705,15 @@ def main():
                              "events on the launch stream around the unprofiled timed loop; "
                              "profiled_kernel_ms = per-launch events in a separate pass"},
         # The build's real ceiling is the VALU: the reference's three 64-bit hashes and
-        # exact remainders alone run at 410-420 Gkeys/s on this chip (tools/ubench.py,
-        # compute only), i.e. 2.2 TB/s = 0.27 of HBM at 5.25 B/key.
-        "compute_ceiling": {"bound": "valu", "unit": "Gkeys/s", "hash_mod_only": 410.0,
+        # exact remainders alone run at 437-446 Gkeys/s on this chip (tools/ubench.py,
+        # compute only), i.e. 2.3 TB/s = 0.29 of HBM at 5.25 B/key.
+        "compute_ceiling": {"bound": "valu", "unit": "Gkeys/s", "hash_mod_only": 437.0,
                             "achieved": round(n / (dev_ms_per_step * 1e-3) / 1e9, 2),
-                            "frac": round(n / (dev_ms_per_step * 1e-3) / 1e9 / 410.0, 4),
-                            "source": "profiles/r01/ubench_primitives.jsonl (hash3+mod_fast)"},
+                            "frac": round(n / (dev_ms_per_step * 1e-3) / 1e9 / 437.0, 4),
+                            "source": "profiles/r02/s3/evidence/ub_prim.log (hash3+mod_fast, m = C2)"},
         "clocks": clocks,
+        "library": {"kernel_sha": library_kernel_sha(),
+                    "matches_sources": library_kernel_sha() == kernel_source_sha()},
         "cpu_baseline": cpu,
         "kernels": kernels,
         "verified_vs_oracle": all_ok if verified is not None or dist else None,

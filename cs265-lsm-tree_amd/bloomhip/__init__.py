@@ -50,7 +50,8 @@ PROF_SLOTS = 10
 
 # Every symbol include/bloomhip.h and include/bloomhip_workload.h declare.
 EXPORTED_SYMBOLS = (
-    "bloomhip_abi_version", "bloomhip_strerror", "bloomhip_last_error", "bloomhip_device_count",
+    "bloomhip_abi_version", "bloomhip_kernel_sha", "bloomhip_strerror", "bloomhip_last_error",
+    "bloomhip_device_count",
     "bloomhip_m_bits", "bloomhip_create", "bloomhip_destroy", "bloomhip_size",
     "bloomhip_nwords", "bloomhip_device", "bloomhip_device_words", "bloomhip_stream",
     "bloomhip_clear", "bloomhip_set_batch", "bloomhip_test_batch", "bloomhip_set",
@@ -97,6 +98,7 @@ def _lib():
         PU64 = ctypes.POINTER(ctypes.c_uint64)
         sig = {
             "bloomhip_abi_version": (I, []),
+            "bloomhip_kernel_sha": (ctypes.c_char_p, []),
             "bloomhip_strerror": (ctypes.c_char_p, [I]),
             "bloomhip_last_error": (ctypes.c_char_p, []),
             "bloomhip_device_count": (I, [ctypes.POINTER(I)]),

@@ -400,6 +400,11 @@ extern "C" {
 
 int bloomhip_abi_version(void) { return BLOOMHIP_ABI_VERSION; }
 
+#ifndef BLOOMHIP_KERNEL_SHA
+#define BLOOMHIP_KERNEL_SHA "unknown"
+#endif
+const char *bloomhip_kernel_sha(void) { return BLOOMHIP_KERNEL_SHA; }
+
 const char *bloomhip_strerror(int status) {
     switch (status) {
         case BLOOMHIP_OK: return "ok";

@@ -75,6 +75,10 @@ extern "C" {
 typedef struct bloomhip_filter bloomhip_filter;
 
 int bloomhip_abi_version(void);
+/* Digest of the kernel sources this library was compiled from (first 16 hex
+ * digits of SHA-256 over csrc/bloom_kernels.hip, bloom_kernels.h,
+ * bloom_math.h): measurement tools tie profiles to the kernels that ran. */
+const char *bloomhip_kernel_sha(void);
 const char *bloomhip_strerror(int status);
 /* Text of the last HIP error seen by this host thread ("" if none). */
 const char *bloomhip_last_error(void);

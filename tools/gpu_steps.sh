@@ -20,6 +20,7 @@ pmc() {  # workload counter benchargs...
   run "pmc_${w}_$c" 150 timeout -s KILL 140 rocprofv3 --pmc "$c" --kernel-trace \
       -d "$OUT/pmc_${w}_$c" -o pmc --output-format csv -- python bench.py "$@"
 }
+python -c "import sys; sys.path.insert(0, '.'); import bench; print('library kernel sha', bench.library_kernel_sha(), 'sources', bench.kernel_source_sha())" 2>/dev/null | tee "$OUT/library.txt"
 for s in ${STEPS//,/ }; do
   case $s in
     pytest) run pytest 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
@@ -28,6 +29,7 @@ for s in ${STEPS//,/ }; do
     bench_quick) run bench_quick 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline || exit 1 ;;
     bench_c4) run bench_c4 400 python bench.py --workload c4 --steps 5 --warmup 1 --no-extras --no-cpu-baseline || exit 1 ;;
     bench_c4w) run bench_c4w 400 python bench.py --workload c4w --steps 5 --warmup 1 --no-extras --no-cpu-baseline || exit 1 ;;
+    ub_prim) run ub_prim 200 python tools/ubench.py || exit 1 ;;
     ub_isa) run ub_isa 120 python tools/ubench_isa.py || exit 1 ;;
     ub_part) run ub_part 300 python tools/ubench.py part || exit 1 ;;
     ub_part_c5) run ub_part_c5 300 python tools/ubench.py part_c5 || exit 1 ;;

@@ -52,7 +52,7 @@ def main(w, tag):
                          "write_bytes": int(write)}
         total += fetch + write
     sys.path.insert(0, ROOT)
-    from bench import kernel_source_sha
+    from bench import library_kernel_sha as kernel_source_sha
     out = {"workload": w, "round": tag, "hbm_bytes_per_build": int(total), "kernels": kernels,
            "kernel_source_sha": kernel_source_sha(),
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
