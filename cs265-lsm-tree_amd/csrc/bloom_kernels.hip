@@ -838,54 +838,63 @@ __global__ void __launch_bounds__(kProbeLdsBlock) k_probe_lds(KeySpan ks, const 
 }
 
 // Partitioned / stacked probe, last step (k_probe_combine): one workgroup per
-// tile stages the tile's result bytes (sorted order) in LDS and, for each key,
-// ANDs the bytes at its three slots; bit j of the AND is filter j's is_set,
-// packed 64 keys per u64 by a 64-lane ballot into row rows.row[j] of out.
-// Each thread owns TILE_KEYS / kCombineBlock keys (lane-consecutive per
-// wave, for the ballot) and issues all of their slot loads before it waits on
-// anything, so a workgroup pays one memory latency, not one per key step.
-// Lane j < nf stores member j's word of each 64-key step.
-constexpr int kCombineBlockDefault = 1024;  // 1024: 42 us at C3, 512: 45, 256: 53
+// tile stages the tile's result bytes (sorted order) in LDS; thread t takes the
+// 8 consecutive keys 8t .. 8t+7, reads their slots as one 16-B vector per hash
+// (8-byte-per-lane loads of round 1 took the address unit 24 instructions per
+// thread), ANDs each key's three bytes (bit j of the AND is filter j's is_set)
+// and writes, per filter j, the byte of its 8 answers: key 8t + i at bit i of
+// byte t of the tile's part of row rows.row[j] (the packed rows' bit order:
+// bit i % 64 of word i / 64 is key i).  A wave's bytes are 64 contiguous bytes
+// per row.  The bits of filter j are gathered out of the 8 AND bytes by two
+// multiplies: with bytes b0..b3 (0/1 at bits 0, 8, 16, 24),
+// (b * 0x01020408) >> 24 puts b_i at bit i and every other partial product
+// below bit 24 or above bit 31 (no carries: those bits are distinct).
+constexpr int kCombineKeys = 8;  // keys per thread
 template <int TILE_KEYS, int kCombineBlock>
 __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, size_t n,
     uint64_t *__restrict__ out, size_t nw, StackTable rows) {
     constexpr int kTilePos = 3 * TILE_KEYS;
-    constexpr int kPer = TILE_KEYS / kCombineBlock;
-    static_assert(kPer * kCombineBlock == TILE_KEYS, "whole key steps");
+    static_assert(kCombineBlock * kCombineKeys == TILE_KEYS, "8 keys per thread");
     __shared__ __attribute__((aligned(16))) uint8_t s_r[kTilePos];
     const size_t tile = blockIdx.x;
     const size_t tile0 = tile * TILE_KEYS;
     const int tile_keys = (int)min((size_t)TILE_KEYS, n - tile0);
-    const uint16_t *sl = slots + tile * 3 * TILE_KEYS;
-    uint32_t sa[kPer], sb[kPer], sc[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; j++) {
-        const int key = j * kCombineBlock + (int)threadIdx.x;
-        const bool live = key < tile_keys;
-        sa[j] = live ? sl[key] : 0u;
-        sb[j] = live ? sl[TILE_KEYS + key] : 0u;
-        sc[j] = live ? sl[2 * TILE_KEYS + key] : 0u;
-    }
+    const int k0 = kCombineKeys * (int)threadIdx.x;  // this thread's first key in the tile
+    const uint4 *sl = reinterpret_cast<const uint4 *>(slots + tile * 3 * TILE_KEYS + k0);
+    const uint4 va = sl[0], vb = sl[TILE_KEYS / 8], vc = sl[2 * (TILE_KEYS / 8)];
     const uint4 *src = reinterpret_cast<const uint4 *>(res + tile * (size_t)kTilePos);
     for (int q = threadIdx.x; q < kTilePos / 16; q += kCombineBlock)
         reinterpret_cast<uint4 *>(s_r)[q] = src[q];
     __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nf = rows.nf;
-    // lane f < nf stores member f's words: its row, this tile's first word
-    uint64_t *dst = out + (size_t)(lane < nf ? rows.row[lane] : 0) * nw + tile0 / 64 + wave;
+    // live keys of a short last tile; past them the slots are stale
+    const uint32_t a[4] = {va.x, va.y, va.z, va.w}, b[4] = {vb.x, vb.y, vb.z, vb.w},
+                   c[4] = {vc.x, vc.y, vc.z, vc.w};
+    uint32_t hit[kCombineKeys];
 #pragma unroll
-    for (int j = 0; j < kPer; j++) {
-        const int key = j * kCombineBlock + (int)threadIdx.x;
-        const uint32_t hit = key < tile_keys ? (uint32_t)(s_r[sa[j]] & s_r[sb[j]] & s_r[sc[j]]) : 0u;
-        const int base = j * kCombineBlock + wave * 64;
-        uint64_t mine = 0;
-        for (int f = 0; f < nf; f++) {
-            const uint64_t ballot = __ballot((hit >> f) & 1u);
-            if (lane == f) mine = ballot;
+    for (int i = 0; i < kCombineKeys; i++) {
+        const int sh = 16 * (i & 1);
+        const uint32_t sa = (a[i / 2] >> sh) & 0xFFFFu, sb = (b[i / 2] >> sh) & 0xFFFFu,
+                       sc = (c[i / 2] >> sh) & 0xFFFFu;
+        hit[i] = k0 + i < tile_keys ? (uint32_t)(s_r[min(sa, (uint32_t)kTilePos - 1)] &
+                                                 s_r[min(sb, (uint32_t)kTilePos - 1)] &
+                                                 s_r[min(sc, (uint32_t)kTilePos - 1)])
+                                    : 0u;
+    }
+    // bytes of the tile's rows that hold keys: whole 64-key words, so the last
+    // word of a short tile gets its zero bits too
+    if (k0 >= ((tile_keys + 63) & ~63)) return;
+    const uint32_t lo = hit[0] | (hit[1] << 8) | (hit[2] << 16) | (hit[3] << 24);
+    const uint32_t hi = hit[4] | (hit[5] << 8) | (hit[6] << 16) | (hit[7] << 24);
+    const size_t byte0 = tile0 / 8 + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kMaxStack; j++) {
+        if (j < rows.nf) {
+            const uint32_t bl = ((lo >> j) & 0x01010101u) * 0x01020408u;
+            const uint32_t bh = ((hi >> j) & 0x01010101u) * 0x01020408u;
+            const uint32_t byte = (bl >> 24) | ((bh >> 20) & 0xF0u);
+            reinterpret_cast<uint8_t *>(out + (size_t)rows.row[j] * nw)[byte0] = (uint8_t)byte;
         }
-        if (lane < nf && base < tile_keys) dst[j * (kCombineBlock / 64)] = mine;
     }
 }
 
@@ -1493,12 +1502,13 @@ hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *word
 hipError_t launch_combine(const PartitionWorkspace &ws, const uint8_t *res, const uint16_t *slots,
                           size_t n, uint64_t *out, size_t nw, const StackTable &rows,
                           hipStream_t stream) {
+    constexpr int kBig = 2 * (int)kPartTileKeys, kSmall = (int)kPartTileKeys;
     if (tile_keys_of(ws) == 2 * kPartTileKeys)
-        k_probe_combine<2 * (int)kPartTileKeys, kCombineBlockDefault>
-            <<<(unsigned)ws.ntiles, kCombineBlockDefault, 0, stream>>>(res, slots, n, out, nw, rows);
+        k_probe_combine<kBig, kBig / kCombineKeys>
+            <<<(unsigned)ws.ntiles, kBig / kCombineKeys, 0, stream>>>(res, slots, n, out, nw, rows);
     else
-        k_probe_combine<(int)kPartTileKeys, kCombineBlockDefault>
-            <<<(unsigned)ws.ntiles, kCombineBlockDefault, 0, stream>>>(res, slots, n, out, nw, rows);
+        k_probe_combine<kSmall, kSmall / kCombineKeys>
+            <<<(unsigned)ws.ntiles, kSmall / kCombineKeys, 0, stream>>>(res, slots, n, out, nw, rows);
     return hipGetLastError();
 }
 
