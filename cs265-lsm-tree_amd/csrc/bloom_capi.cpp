@@ -198,6 +198,8 @@ struct Workspace {
     size_t msplit_bytes = 0;
     uint32_t *mcount = nullptr;  // compaction: block counts / offsets
     size_t mcount_bytes = 0;
+    int32_t *mkeys = nullptr;  // compaction: the merged run's kept keys, packed
+    size_t mkeys_bytes = 0;
 };
 
 std::mutex g_ws_mu;
@@ -613,8 +615,10 @@ int bloomhip_set_batch(bloomhip_filter *f, const void *keys, size_t n, size_t st
 namespace {
 
 // bloomhip_set_batch_run with f->mu held and f's device current.
+// sorted: the caller guarantees keys ascending (a compaction's output), so the
+// max key is the last one and only the fence keys need reading.
 int set_batch_run_locked(bloomhip_filter *f, const void *keys, size_t n, size_t stride_bytes,
-                         int keys_on_device, hipStream_t s) {
+                         int keys_on_device, hipStream_t s, bool sorted = false) {
     KeySpan ks{};
     int rc = device_keys(f, keys, n, stride_bytes, keys_on_device, s, &ks);
     if (rc) return rc;
@@ -626,7 +630,7 @@ int set_batch_run_locked(bloomhip_filter *f, const void *keys, size_t n, size_t 
     if (nf > 0xFFFFFFFFull) return BLOOMHIP_ERANGE;
     rc = meta_reserve(f, nf);
     if (rc) return rc;
-    hipError_t e = launch_run_meta(ks, f->d_meta, s);
+    hipError_t e = sorted ? launch_run_meta_sorted(ks, f->d_meta, s) : launch_run_meta(ks, f->d_meta, s);
     if (e != hipSuccess) return fail_hip(e, "k_run_meta launch");
     f->nfences = (uint32_t)nf;
     if (!keys_on_device) HIP_TRY(hipStreamSynchronize(s));
@@ -1130,7 +1134,8 @@ int bloomhip_trim(void) {
         DeviceGuard g(kv.first.first);
         (void)hipStreamSynchronize(kv.first.second);
         for (void *p : {(void *)w->pos, (void *)w->runs, (void *)w->res, (void *)w->slots,
-                        w->mbuf[0], w->mbuf[1], (void *)w->msplit, (void *)w->mcount})
+                        w->mbuf[0], w->mbuf[1], (void *)w->msplit, (void *)w->mcount,
+                        (void *)w->mkeys})
             if (p) (void)hipFree(p);
     }
     g_ws.clear();
@@ -1170,6 +1175,9 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
                              merge_split_words(total) * 8, s));
         HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->mcount), &w->mcount_bytes,
                              compact_count_words(total) * 4 + 4, s));
+        if (f)
+            HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->mkeys), &w->mkeys_bytes,
+                                 std::max<uint64_t>(total, 1) * 4, s));
         // the runs, newest first; host runs are staged into mbuf[0]
         std::vector<std::pair<const char *, uint64_t>> list;
         uint64_t off = 0;
@@ -1212,7 +1220,10 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
         const char *merged = list.empty() ? nullptr : list[0].first;
         void *dst = out_on_device ? out_entries : w->mbuf[merged == w->mbuf[0] ? 1 : 0];
         if (merged) {
-            hipError_t e = launch_dedup(merged, total, drop_tombstones, dst, w->mcount, s);
+            // with a filter to build, the kept keys also go out packed: the
+            // build's pass 1 then reads 4 B per key, not the 8-B entries
+            hipError_t e = launch_dedup(merged, total, drop_tombstones, dst, w->mcount, s,
+                                        f ? w->mkeys : nullptr);
             if (e != hipSuccess) return fail_hip(e, "dedup launch");
             uint32_t cnt = 0;
             HIP_TRY(hipMemcpyAsync(&cnt, w->mcount + compact_count_words(total) - 1, 4,
@@ -1221,7 +1232,9 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
             kept = cnt;
         }
         if (f) {
-            int rc = set_batch_run_locked(f, dst, (size_t)kept, 8, 1, s);
+            // the merged run is sorted by key: fences and max key directly
+            int rc = kept ? set_batch_run_locked(f, w->mkeys, (size_t)kept, 4, 1, s, true)
+                          : set_batch_run_locked(f, dst, 0, 8, 1, s, true);
             if (rc) return rc;
         }
         if (!out_on_device && kept)

@@ -187,6 +187,8 @@ hipError_t launch_is_set1(const uint32_t *words, const ModParams &mp, int32_t ke
                           hipStream_t stream);
 // meta[0] = max key, meta[1 ..] = the ceil(n / kFenceStride) fences of a run.
 hipError_t launch_run_meta(const KeySpan &keys, int32_t *meta, hipStream_t stream);
+// The same for keys known sorted ascending: fences read directly, max = last key.
+hipError_t launch_run_meta_sorted(const KeySpan &keys, int32_t *meta, hipStream_t stream);
 // Applies the range checks to the probe rows `cand` in place and writes the
 // newest candidate run and its page index per key (first/page may be null).
 hipError_t launch_route(const KeySpan &keys, const RouteTable &t, uint64_t *cand, size_t nw,

@@ -1581,6 +1581,31 @@ hipError_t launch_probe_lds(const KeySpan &ks, const ModParams &mp, const uint32
     return hipGetLastError();
 }
 
+// A run known to be sorted by key (a compaction's output): its max key is
+// the last key, and only the fence keys are read (src/run.cpp:164-170 give the
+// same values for a run written in key order).
+template <int LAYOUT>
+__global__ void __launch_bounds__(kMetaBlock) k_run_meta_sorted(KeySpan ks, size_t nf,
+                                                                int32_t *__restrict__ meta) {
+    const size_t i = (size_t)blockIdx.x * kMetaBlock + threadIdx.x;
+    if (i < nf) meta[1 + i] = load_key<LAYOUT>(ks, i * kFenceStride);
+    if (i == 0) meta[0] = load_key<LAYOUT>(ks, ks.n - 1);
+}
+
+hipError_t launch_run_meta_sorted(const KeySpan &ks, int32_t *meta, hipStream_t stream) {
+    if (ks.n == 0)
+        return hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(meta), (int)INT32_MIN, 1, stream);
+    const size_t nf = (ks.n + kFenceStride - 1) / kFenceStride;
+    const unsigned grid = (unsigned)((nf + kMetaBlock - 1) / kMetaBlock);
+    if (ks.layout == KEYS_PACKED)
+        k_run_meta_sorted<KEYS_PACKED><<<grid, kMetaBlock, 0, stream>>>(ks, nf, meta);
+    else if (ks.layout == KEYS_ENTRY)
+        k_run_meta_sorted<KEYS_ENTRY><<<grid, kMetaBlock, 0, stream>>>(ks, nf, meta);
+    else
+        k_run_meta_sorted<KEYS_STRIDED><<<grid, kMetaBlock, 0, stream>>>(ks, nf, meta);
+    return hipGetLastError();
+}
+
 hipError_t launch_run_meta(const KeySpan &ks, int32_t *meta, hipStream_t stream) {
     hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(meta), (int)INT32_MIN, 1,
                                      stream);

@@ -15,8 +15,9 @@ uint64_t merge_split_words(uint64_t total);
 // Keeps the first entry of each key of a key-sorted array (dropping entries
 // whose value is VAL_TOMBSTONE when drop_tombstones), packed into out; the
 // kept count lands in counts_ws[ceil(n / tile)] (compact_count_words(n) u32).
+// keys_out (optional, n int32): the kept keys, packed.
 hipError_t launch_dedup(const void *in, uint64_t n, int drop_tombstones, void *out,
-                        uint32_t *counts_ws, hipStream_t stream);
+                        uint32_t *counts_ws, hipStream_t stream, int32_t *keys_out = nullptr);
 uint64_t compact_count_words(uint64_t n);
 
 }  // namespace bloomhip

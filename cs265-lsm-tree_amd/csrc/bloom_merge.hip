@@ -186,9 +186,11 @@ __global__ void __launch_bounds__(1024) k_scan_counts(uint32_t *__restrict__ cou
 // Kept entries leave in input order: per round, an exclusive scan of the
 // lanes' kept counts places them, so a wave's stores cover one contiguous
 // range of the output.
+// keys_out (optional): the kept keys again, packed (stride 4), for the new
+// run's filter build (pass 1 reads 4 B per key instead of 8).
 __global__ void __launch_bounds__(kCompactBlock) k_compact_write(
     const Entry *__restrict__ e, uint64_t n, int drop, const uint32_t *__restrict__ offsets,
-    Entry *__restrict__ out) {
+    Entry *__restrict__ out, int32_t *__restrict__ keys_out) {
     __shared__ uint32_t s_w[kCompactBlock / 64];
     const uint64_t base = (uint64_t)blockIdx.x * kCompactTile + 2 * (uint64_t)threadIdx.x;
     Pair p[kCompactRounds];
@@ -202,6 +204,10 @@ __global__ void __launch_bounds__(kCompactBlock) k_compact_write(
         const uint64_t pos = run + block_exclusive_scan(p[r].k0 + p[r].k1, s_w, &total);
         if (p[r].k0) out[pos] = p[r].e0;
         if (p[r].k1) out[pos + p[r].k0] = p[r].e1;
+        if (keys_out) {
+            if (p[r].k0) keys_out[pos] = p[r].e0.key;
+            if (p[r].k1) keys_out[pos + p[r].k0] = p[r].e1.key;
+        }
         run += total;
     }
 }
@@ -228,7 +234,7 @@ uint64_t merge_split_words(uint64_t total) { return total / kMergeTile + 2; }
 uint64_t compact_count_words(uint64_t n) { return (n + kCompactTile - 1) / kCompactTile + 1; }
 
 hipError_t launch_dedup(const void *in, uint64_t n, int drop_tombstones, void *out,
-                        uint32_t *counts_ws, hipStream_t stream) {
+                        uint32_t *counts_ws, hipStream_t stream, int32_t *keys_out) {
     const uint64_t nblocks = (n + kCompactTile - 1) / kCompactTile;
     const Entry *e = reinterpret_cast<const Entry *>(in);
     if (nblocks) {
@@ -241,7 +247,7 @@ hipError_t launch_dedup(const void *in, uint64_t n, int drop_tombstones, void *o
     hipError_t err = hipGetLastError();
     if (err != hipSuccess || nblocks == 0) return err;
     k_compact_write<<<(unsigned)nblocks, kCompactBlock, 0, stream>>>(
-        e, n, drop_tombstones, counts_ws, reinterpret_cast<Entry *>(out));
+        e, n, drop_tombstones, counts_ws, reinterpret_cast<Entry *>(out), keys_out);
     return hipGetLastError();
 }
 

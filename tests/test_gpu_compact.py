@@ -67,3 +67,30 @@ def test_compact_device_buffers(coracle):
     want = coracle.compact(runs, False)
     assert np.array_equal(got.cpu().numpy(), want)
     assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()
+
+
+@pytest.mark.parametrize("sizes", [[1], [4096], [4097], [8192, 1], [12_289, 4095, 3]])
+def test_compact_filter_and_fences_at_fence_boundaries(coracle, sizes):
+    # the compaction builds its filter from the kept keys (packed) and reads
+    # the sorted run's fences + last key directly: fence counts around 4096
+    runs = make_runs(sizes, 2**31 - 1, sum(sizes) % 1009, tomb_frac=0.0)
+    total = sum(r.shape[0] for r in runs)
+    f = bh.BloomFilter(bh.m_bits(max(total, 1), 10.0))
+    got = bh.compact(runs, drop_tombstones=True, filter=f)
+    want = coracle.compact(runs, True)
+    assert np.array_equal(got, want)
+    assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()
+    fences, mk = f.run_meta()
+    wf, wmk = coracle.run_meta(want[:, 0].copy())
+    assert np.array_equal(fences, wf) and mk == wmk
+
+
+def test_compact_everything_dropped_leaves_an_empty_run(coracle):
+    runs = [np.array([[5, TOMB], [9, TOMB]], dtype=np.int32),
+            np.array([[5, 1], [9, 2]], dtype=np.int32)]
+    f = bh.BloomFilter(bh.m_bits(4, 10.0))
+    got = bh.compact(runs, drop_tombstones=True, filter=f)
+    assert got.shape[0] == 0 and np.array_equal(got.reshape(-1, 2), coracle.compact(runs, True))
+    assert not f.words().any()
+    fences, mk = f.run_meta()
+    assert fences.size == 0 and mk == np.iinfo(np.int32).min
