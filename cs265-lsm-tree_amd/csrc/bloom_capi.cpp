@@ -1169,7 +1169,8 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
         if (f) flk = std::unique_lock<std::mutex>(f->mu);
         Workspace *w = workspace_for(device, s);
         std::lock_guard<std::recursive_mutex> wl(w->mu);
-        const size_t bytes = std::max<uint64_t>(total, 1) * 8;
+        // + one entry of padding per run: merge outputs start 16-B aligned
+        const size_t bytes = (std::max<uint64_t>(total, 1) + (uint64_t)nruns + 2) * 8;
         for (int i = 0; i < 2; i++) HIP_TRY(grow_touched(&w->mbuf[i], &w->mbuf_bytes[i], bytes, s));
         HIP_TRY(grow_touched(reinterpret_cast<void **>(&w->msplit), &w->msplit_bytes,
                              merge_split_words(total) * 8, s));
@@ -1211,7 +1212,7 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
                                            hipMemcpyDeviceToDevice, s));
                     next.push_back({dst, list[i].second});
                 }
-                o += next.back().second;
+                o += (next.back().second + 1) & ~1ull;  // every output 16-B aligned
             }
             list.swap(next);
             dst_buf ^= 1;

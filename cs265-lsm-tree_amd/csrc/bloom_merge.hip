@@ -48,10 +48,12 @@ __device__ __forceinline__ uint64_t merge_path(GetA a_key, uint64_t na, GetB b_k
     return lo;
 }
 
-// One thread per tile boundary, a binary merge-path search.  (A 64-ary
-// search by one wave per boundary, 4 rounds instead of 23 dependent loads,
-// was slower at C3's fan-in: 31 vs 22 us, since its 128 scattered loads per
-// round miss where the serial searches' first levels share cached lines.)
+// One thread per tile boundary, a binary merge-path search.  (Wider searches
+// were slower: a 64-ary search by one wave per boundary 31 vs 22 us, its 128
+// scattered loads per round missing where the serial searches' first levels
+// share cached lines; a 16-ary search by one thread, 15 probes per round,
+// 79 vs 23 us: 30 scattered loads per round and thread queue in the address
+// units of the few CUs the 33 workgroups occupy.)
 __global__ void k_merge_split(const Entry *__restrict__ a, uint64_t na,
                               const Entry *__restrict__ b, uint64_t nb, uint64_t ntiles,
                               uint64_t *__restrict__ split) {
@@ -62,26 +64,55 @@ __global__ void k_merge_split(const Entry *__restrict__ a, uint64_t na,
                           [&](uint64_t j) { return b[j].key; }, nb, d);
 }
 
+// A merge tile: the tile's share of A and of B staged in LDS, one merge-path
+// search per lane in LDS, 8 outputs per lane, the tile written back.  Global
+// traffic moves in 16-B vectors: a share is copied in the 16-B-aligned
+// vectors (by address) that cover it and lands at the same parity in LDS;
+// a vector that reaches outside its array is copied entry by entry.  The
+// output tile starts at an even entry of a 16-B-aligned output (launch_merge2
+// checks) and leaves as 16-B stores.
+// Entries s0 .. s0+cnt-1 of src go to dst[par + k], par = the address parity
+// of src + s0 (in entries); dst is 16-B aligned.
+__device__ __forceinline__ void stage_share(const Entry *__restrict__ src, uint64_t n,
+                                            uint64_t s0, int cnt, int par, Entry *dst) {
+    if (cnt <= 0) return;
+    const int nv = (par + cnt + 1) / 2;
+    int4 *d4 = reinterpret_cast<int4 *>(dst);
+    for (int v = threadIdx.x; v < nv; v += kMergeBlock) {
+        const int64_t e = (int64_t)s0 - par + 2 * (int64_t)v;  // the vector's first entry
+        if (e >= 0 && (uint64_t)e + 1 < n) {
+            d4[v] = *reinterpret_cast<const int4 *>(src + e);
+        } else {
+            if (e >= 0 && (uint64_t)e < n) dst[2 * v] = src[e];
+            if (e + 1 >= 0 && (uint64_t)(e + 1) < n) dst[2 * v + 1] = src[e + 1];
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kMergeBlock) k_merge_tile(const Entry *__restrict__ a,
                                                             uint64_t na,
                                                             const Entry *__restrict__ b,
                                                             uint64_t nb,
                                                             const uint64_t *__restrict__ split,
                                                             Entry *__restrict__ out) {
-    __shared__ Entry s_in[kMergeTile];
-    __shared__ Entry s_out[kMergeTile];
+    __shared__ __attribute__((aligned(16))) Entry s_in[kMergeTile + 4];
+    __shared__ __attribute__((aligned(16))) Entry s_out[kMergeTile];
     const uint64_t t = blockIdx.x;
     const uint64_t d0 = t * kMergeTile, d1 = min(d0 + kMergeTile, na + nb);
     const uint64_t a0 = split[t], a1 = split[t + 1];
     const uint64_t b0 = d0 - a0, b1 = d1 - a1;
     const int ta = (int)(a1 - a0), tb = (int)(b1 - b0);
-    for (int i = threadIdx.x; i < ta; i += kMergeBlock) s_in[i] = a[a0 + i];
-    for (int i = threadIdx.x; i < tb; i += kMergeBlock) s_in[ta + i] = b[b0 + i];
+    const int pa = (int)((reinterpret_cast<uintptr_t>(a + a0) >> 3) & 1);  // A at s_in[pa]
+    const int pbp = (int)((reinterpret_cast<uintptr_t>(b + b0) >> 3) & 1);
+    const int bb = (pa + ta + 1) & ~1;  // B's vectors from here
+    const int pb = bb + pbp;            // B at s_in[pb]
+    stage_share(a, na, a0, ta, pa, s_in);
+    stage_share(b, nb, b0, tb, pbp, s_in + bb);
     __syncthreads();
     const int d = threadIdx.x * kMergeIpt;
     const int total = ta + tb;
     if (d < total) {
-        const Entry *sa = s_in, *sb = s_in + ta;
+        const Entry *sa = s_in + pa, *sb = s_in + pb;
         int ia = (int)merge_path([&](uint64_t i) { return sa[i].key; }, (uint64_t)ta,
                                  [&](uint64_t j) { return sb[j].key; }, (uint64_t)tb, (uint64_t)d);
         int ib = d - ia;
@@ -92,7 +123,10 @@ __global__ void __launch_bounds__(kMergeBlock) k_merge_tile(const Entry *__restr
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < total; i += kMergeBlock) out[d0 + i] = s_out[i];
+    int4 *o4 = reinterpret_cast<int4 *>(out + d0);  // d0 even, out 16-B aligned
+    const int4 *s4 = reinterpret_cast<const int4 *>(s_out);
+    for (int i = threadIdx.x; i < total / 2; i += kMergeBlock) o4[i] = s4[i];
+    if ((total & 1) && threadIdx.x == 0) out[d0 + total - 1] = s_out[total - 1];
 }
 
 // Keep entry i when it is the first (newest) of its key, and not a dropped
@@ -221,6 +255,10 @@ hipError_t launch_merge2(const void *a, uint64_t na, const void *b, uint64_t nb,
     const uint64_t ntiles = (total + kMergeTile - 1) / kMergeTile;
     const Entry *ea = reinterpret_cast<const Entry *>(a);
     const Entry *eb = reinterpret_cast<const Entry *>(b);
+    // inputs 8-B aligned (entries), the output 16-B aligned (vector stores)
+    if (((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 7) ||
+        (reinterpret_cast<uintptr_t>(out) & 15))
+        return hipErrorInvalidValue;
     k_merge_split<<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, stream>>>(ea, na, eb, nb, ntiles,
                                                                           split_ws);
     hipError_t e = hipGetLastError();

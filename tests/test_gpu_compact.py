@@ -94,3 +94,21 @@ def test_compact_everything_dropped_leaves_an_empty_run(coracle):
     assert not f.words().any()
     fences, mk = f.run_meta()
     assert fences.size == 0 and mk == np.iinfo(np.int32).min
+
+
+def test_compact_device_runs_at_odd_entry_offsets(coracle):
+    # device runs that start 8 B past a 16-B boundary: the merge stages each
+    # share in address-aligned 16-B vectors at the matching LDS parity
+    torch = pytest.importorskip("torch")
+    runs = make_runs([70_001, 33_333, 4097, 2], 2**31 - 1, 11)
+    views = []
+    for r in runs:
+        buf = torch.zeros((r.shape[0] + 2, 2), dtype=torch.int32, device="cuda")
+        buf[1:1 + r.shape[0]] = torch.from_numpy(r).cuda()
+        views.append(buf[1:1 + r.shape[0]])
+    assert all((v.data_ptr() % 16) == 8 for v in views)
+    f = bh.BloomFilter(bh.m_bits(sum(r.shape[0] for r in runs), 10.0))
+    got = bh.compact(views, drop_tombstones=False, filter=f)
+    want = coracle.compact(runs, False)
+    assert np.array_equal(np.asarray(got), want)
+    assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()
