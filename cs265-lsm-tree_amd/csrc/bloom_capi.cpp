@@ -1200,12 +1200,14 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
             std::vector<std::pair<const char *, uint64_t>> next;
             char *base = static_cast<char *>(w->mbuf[dst_buf]);
             uint64_t o = 0;
+            // the round's merges go out together (one split + one tile
+            // launch per kMaxMergePairs pairs)
+            std::vector<MergePairArgs> pairs;
             for (size_t i = 0; i < list.size(); i += 2) {
                 char *dst = base + o * 8;
                 if (i + 1 < list.size()) {
-                    hipError_t e = launch_merge2(list[i].first, list[i].second, list[i + 1].first,
-                                                 list[i + 1].second, dst, w->msplit, s);
-                    if (e != hipSuccess) return fail_hip(e, "merge launch");
+                    pairs.push_back({list[i].first, list[i].second, list[i + 1].first,
+                                     list[i + 1].second, dst});
                     next.push_back({dst, list[i].second + list[i + 1].second});
                 } else {
                     HIP_TRY(hipMemcpyAsync(dst, list[i].first, list[i].second * 8,
@@ -1213,6 +1215,11 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
                     next.push_back({dst, list[i].second});
                 }
                 o += (next.back().second + 1) & ~1ull;  // every output 16-B aligned
+            }
+            for (size_t p0 = 0; p0 < pairs.size(); p0 += kMaxMergePairs) {
+                const int np = (int)std::min<size_t>(kMaxMergePairs, pairs.size() - p0);
+                hipError_t e = launch_merge_round(pairs.data() + p0, np, w->msplit, s);
+                if (e != hipSuccess) return fail_hip(e, "merge launch");
             }
             list.swap(next);
             dst_buf ^= 1;

@@ -7,9 +7,22 @@
 namespace bloomhip {
 
 // Stable merge of two key-sorted entry_t arrays (a wins ties) into out
-// (na + nb entries).  split_ws: merge_split_words(na + nb) u64.
+// (na + nb entries; a, b 8-B aligned, out 16-B aligned).  split_ws:
+// merge_split_words(na + nb) u64.
 hipError_t launch_merge2(const void *a, uint64_t na, const void *b, uint64_t nb, void *out,
                          uint64_t *split_ws, hipStream_t stream);
+// Up to kMaxMergePairs such merges in one pair of launches (a merge round);
+// split_ws: merge_split_words(total entries of the round) u64.
+constexpr int kMaxMergePairs = 8;
+struct MergePairArgs {
+    const void *a;
+    uint64_t na;
+    const void *b;
+    uint64_t nb;
+    void *out;
+};
+hipError_t launch_merge_round(const MergePairArgs *pairs, int np, uint64_t *split_ws,
+                              hipStream_t stream);
 uint64_t merge_split_words(uint64_t total);
 
 // Keeps the first entry of each key of a key-sorted array (dropping entries

@@ -54,12 +54,29 @@ __device__ __forceinline__ uint64_t merge_path(GetA a_key, uint64_t na, GetB b_k
 // share cached lines; a 16-ary search by one thread, 15 probes per round,
 // 79 vs 23 us: 30 scattered loads per round and thread queue in the address
 // units of the few CUs the 33 workgroups occupy.)
-__global__ void k_merge_split(const Entry *__restrict__ a, uint64_t na,
-                              const Entry *__restrict__ b, uint64_t nb, uint64_t ntiles,
-                              uint64_t *__restrict__ split) {
+// The pairs of one merge round, launched together (their tiles and split
+// searches share one grid: a round of fan-in 4 pays one split latency, not
+// two).  Pair p's tiles are [tile0[p], tile0[p + 1]); its splits sit at
+// split_ws[tile0[p] + p ..] (ntiles_p + 1 of them).
+struct MergeRound {
+    const Entry *a[kMaxMergePairs];
+    const Entry *b[kMaxMergePairs];
+    Entry *out[kMaxMergePairs];
+    uint64_t na[kMaxMergePairs], nb[kMaxMergePairs];
+    uint64_t tile0[kMaxMergePairs + 1];
+    int np;
+};
+
+__global__ void k_merge_split(MergeRound R, uint64_t *__restrict__ split) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    const uint64_t d = min(t * (uint64_t)kMergeTile, na + nb);
+    if (t >= R.tile0[R.np] + (uint64_t)R.np) return;
+    int p = 0;
+    for (int q = 1; q < R.np; q++)
+        if (R.tile0[q] + (uint64_t)q <= t) p = q;
+    const uint64_t lt = t - (R.tile0[p] + (uint64_t)p);  // boundary lt of pair p
+    const Entry *a = R.a[p], *b = R.b[p];
+    const uint64_t na = R.na[p], nb = R.nb[p];
+    const uint64_t d = min(lt * (uint64_t)kMergeTile, na + nb);
     split[t] = merge_path([&](uint64_t i) { return a[i].key; }, na,
                           [&](uint64_t j) { return b[j].key; }, nb, d);
 }
@@ -89,15 +106,19 @@ __device__ __forceinline__ void stage_share(const Entry *__restrict__ src, uint6
     }
 }
 
-__global__ void __launch_bounds__(kMergeBlock) k_merge_tile(const Entry *__restrict__ a,
-                                                            uint64_t na,
-                                                            const Entry *__restrict__ b,
-                                                            uint64_t nb,
-                                                            const uint64_t *__restrict__ split,
-                                                            Entry *__restrict__ out) {
+__global__ void __launch_bounds__(kMergeBlock) k_merge_tile(MergeRound R,
+                                                            const uint64_t *__restrict__ splits) {
     __shared__ __attribute__((aligned(16))) Entry s_in[kMergeTile + 4];
     __shared__ __attribute__((aligned(16))) Entry s_out[kMergeTile];
-    const uint64_t t = blockIdx.x;
+    int p = 0;
+    for (int q = 1; q < R.np; q++)
+        if (R.tile0[q] <= blockIdx.x) p = q;
+    const Entry *__restrict__ a = R.a[p];
+    const Entry *__restrict__ b = R.b[p];
+    Entry *__restrict__ out = R.out[p];
+    const uint64_t na = R.na[p], nb = R.nb[p];
+    const uint64_t *split = splits + R.tile0[p] + p;
+    const uint64_t t = blockIdx.x - R.tile0[p];
     const uint64_t d0 = t * kMergeTile, d1 = min(d0 + kMergeTile, na + nb);
     const uint64_t a0 = split[t], a1 = split[t + 1];
     const uint64_t b0 = d0 - a0, b1 = d1 - a1;
@@ -248,27 +269,43 @@ __global__ void __launch_bounds__(kCompactBlock) k_compact_write(
 
 }  // namespace
 
-hipError_t launch_merge2(const void *a, uint64_t na, const void *b, uint64_t nb, void *out,
-                         uint64_t *split_ws, hipStream_t stream) {
-    const uint64_t total = na + nb;
-    if (total == 0) return hipSuccess;
-    const uint64_t ntiles = (total + kMergeTile - 1) / kMergeTile;
-    const Entry *ea = reinterpret_cast<const Entry *>(a);
-    const Entry *eb = reinterpret_cast<const Entry *>(b);
-    // inputs 8-B aligned (entries), the output 16-B aligned (vector stores)
-    if (((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 7) ||
-        (reinterpret_cast<uintptr_t>(out) & 15))
-        return hipErrorInvalidValue;
-    k_merge_split<<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, stream>>>(ea, na, eb, nb, ntiles,
-                                                                          split_ws);
+hipError_t launch_merge_round(const MergePairArgs *pairs, int np, uint64_t *split_ws,
+                              hipStream_t stream) {
+    if (np < 1 || np > kMaxMergePairs) return hipErrorInvalidValue;
+    MergeRound R{};
+    R.np = np;
+    uint64_t tiles = 0;
+    for (int p = 0; p < np; p++) {
+        // inputs 8-B aligned (entries), the output 16-B aligned (vector stores)
+        if (((reinterpret_cast<uintptr_t>(pairs[p].a) | reinterpret_cast<uintptr_t>(pairs[p].b)) &
+             7) ||
+            (reinterpret_cast<uintptr_t>(pairs[p].out) & 15))
+            return hipErrorInvalidValue;
+        R.a[p] = reinterpret_cast<const Entry *>(pairs[p].a);
+        R.b[p] = reinterpret_cast<const Entry *>(pairs[p].b);
+        R.out[p] = reinterpret_cast<Entry *>(pairs[p].out);
+        R.na[p] = pairs[p].na;
+        R.nb[p] = pairs[p].nb;
+        R.tile0[p] = tiles;
+        tiles += (pairs[p].na + pairs[p].nb + kMergeTile - 1) / kMergeTile;
+    }
+    R.tile0[np] = tiles;
+    if (tiles == 0) return hipSuccess;
+    const uint64_t nsplit = tiles + (uint64_t)np;
+    k_merge_split<<<(unsigned)((nsplit + 255) / 256), 256, 0, stream>>>(R, split_ws);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    k_merge_tile<<<(unsigned)ntiles, kMergeBlock, 0, stream>>>(ea, na, eb, nb, split_ws,
-                                                               reinterpret_cast<Entry *>(out));
+    k_merge_tile<<<(unsigned)tiles, kMergeBlock, 0, stream>>>(R, split_ws);
     return hipGetLastError();
 }
 
-uint64_t merge_split_words(uint64_t total) { return total / kMergeTile + 2; }
+hipError_t launch_merge2(const void *a, uint64_t na, const void *b, uint64_t nb, void *out,
+                         uint64_t *split_ws, hipStream_t stream) {
+    const MergePairArgs p{a, na, b, nb, out};
+    return launch_merge_round(&p, 1, split_ws, stream);
+}
+
+uint64_t merge_split_words(uint64_t total) { return total / kMergeTile + 2 * kMaxMergePairs + 2; }
 uint64_t compact_count_words(uint64_t n) { return (n + kCompactTile - 1) / kCompactTile + 1; }
 
 hipError_t launch_dedup(const void *in, uint64_t n, int drop_tombstones, void *out,
