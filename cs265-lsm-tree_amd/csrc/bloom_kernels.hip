@@ -9,15 +9,21 @@
 //
 // Build strategies:
 //   atomic    — one pass, 3 global atomicOr per key (any m).
-//   lds       — m/8 <= 64 KiB: every workgroup builds a private copy of the
+//   lds       — m/8 <= 160 KiB: every workgroup builds a private copy of the
 //               whole filter in LDS with ds_or, then ORs its non-zero words
 //               into the global bitmap.
-//   partition — m <= 2^30: pass 1 hashes a tile of keys and counting-sorts
-//               its 3 positions by 2^19-bit segment in LDS, writing the sorted
-//               tile and its per-segment run starts; pass 2 gives every
-//               segment to one workgroup, which gathers that segment's run
-//               from every tile, ORs it into a 64 KiB LDS image and writes
-//               the segment out with coalesced stores.  No global atomics.
+//   partition — m <= 2^33: pass 1 hashes a tile of keys (4096 or 8192) and
+//               counting-sorts its 3 positions by segment in LDS (segments of
+//               up to 160 KiB, a multiple of the CU count where possible),
+//               writing the sorted tile as 21-bit entries packed three per
+//               u64 and its per-segment run starts; pass 2 gives every
+//               segment to one workgroup, which walks that segment's run in
+//               every tile, ORs it into an LDS image of the segment and
+//               writes the segment out with coalesced stores.  No global
+//               atomics.
+// Probe strategies: gather, LDS, partitioned (pass 1 with slots, pass 2 tests
+// the segment's bits, k_probe_combine) and stacked (several filters in one
+// partitioned pass).
 #include "bloom_kernels.h"
 
 #include <stdlib.h>
