@@ -162,6 +162,14 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// (a << S) | b in one instruction.
+template <typename S>
+__device__ __forceinline__ uint32_t lshl_or(uint32_t a, S sh, uint32_t b) {
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(sh), "v"(b));
+    return r;
+}
+
 // Workgroup barrier that waits for this wave's LDS operations only.
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -352,8 +360,12 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
         }
         lds_barrier();
         if constexpr (COLS) {
-            for (int b = tid; b <= nb; b += TB)
-                runs[(size_t)b * ntiles + tile] = (s_hist[b] + ((uint32_t)b << kBinShift)) >> 2;
+            // one bin per thread at C2: a plain loop (the vectorised form the
+            // compiler picked by default costs its setup on every tile)
+            uint32_t *col = runs + (size_t)tid * ntiles + tile;
+#pragma clang loop unroll(disable) vectorize(disable)
+            for (int b = tid; b <= nb; b += TB, col += (size_t)TB * ntiles)
+                *col = (s_hist[b] + ((uint32_t)b << kBinShift)) >> 2;
         } else {
             uint32_t *row = runs + tile * (size_t)(nb + 1);
             for (int b = tid; b <= nb; b += TB) row[b] = (s_hist[b] + ((uint32_t)b << kBinShift)) >> 2;
@@ -417,8 +429,10 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
 #pragma unroll
                 for (int q = 0; q < 6; q++) e[q] &= kEntryMask;
             }
-            v[r] = make_uint4(e[0] | (e[1] << 21), (e[1] >> 11) | (e[2] << 10),
-                              e[3] | (e[4] << 21), (e[4] >> 11) | (e[5] << 10));
+            // (a << s) | b is one v_lshl_or_b32; the compiler emitted a shift
+            // and an or for each (5 instead of 3 per u64)
+            v[r] = make_uint4(lshl_or(e[1], 21, e[0]), lshl_or(e[2], 10, e[1] >> 11),
+                              lshl_or(e[4], 21, e[3]), lshl_or(e[5], 10, e[4] >> 11));
         }
 #pragma unroll
         for (int r = 0; r < kStores; r++) dst[r * TB + tid] = v[r];
