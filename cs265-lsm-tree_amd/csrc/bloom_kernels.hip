@@ -393,8 +393,8 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                 if (FULL) {
                     uint32_t w[kPartKPT / 2];
 #pragma unroll
-                    for (int q = 0; q < kPartKPT / 2; q++)
-                        w[q] = (slot[2 * q] >> 2) | ((slot[2 * q + 1] >> 2) << 16);
+                    for (int q = 0; q < kPartKPT / 2; q++)  // slots are byte offsets: 4 | slot
+                        w[q] = lshl_or(slot[2 * q + 1], 14, slot[2 * q] >> 2);
                     // non-temporal: the slots are read once, by the combine
                     // after pass 2, and kept out of the caches they leave the
                     // sorted entries pass 2 is about to read (C3 pass 1

@@ -51,6 +51,8 @@ def main(w, tag):
         kernels[base] = {"name": f[base][1], "grid": f[base][0], "fetch_bytes": int(fetch),
                          "write_bytes": int(write)}
         total += fetch + write
+    if not kernels:  # a pass is missing (e.g. the GPU call failed): keep the old summary
+        sys.exit(f"pmc_traffic: no build kernels in gpurun_out/{tag}/pmc_{w}_*; nothing written")
     sys.path.insert(0, ROOT)
     from bench import library_kernel_sha as kernel_source_sha
     out = {"workload": w, "round": tag, "hbm_bytes_per_build": int(total), "kernels": kernels,
