@@ -213,3 +213,17 @@ def test_engine_wide_mod_random_m(fuzz_keys):
             continue
         assert (bh.host_positions(int(m), fuzz_keys[:3000]) ==
                 np_positions(fuzz_keys[:3000], int(m))).all(), m
+
+
+def test_library_is_built_from_these_kernel_sources():
+    # the in-tree library carries the digest of the kernel sources it was
+    # compiled from: a stale lib/ (sources edited, not rebuilt) fails here
+    # before any GPU run measures the wrong kernels
+    import hashlib
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    h = hashlib.sha256()
+    for name in ("bloom_kernels.hip", "bloom_kernels.h", "bloom_math.h"):
+        with open(os.path.join(root, "cs265-lsm-tree_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    assert bh.lib().bloomhip_kernel_sha().decode() == h.hexdigest()[:16]
