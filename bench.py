@@ -79,6 +79,17 @@ def host_cpu_info():
     return info
 
 
+def usable_cpus(info):
+    """The CPUs this process can actually run on: min(nproc, affinity mask,
+    cgroup CPU quota) — the box shows 256 CPUs but grants a 16-CPU quota."""
+    c = [info["host_cpus"] or 1]
+    if info.get("affinity_cpus"):
+        c.append(info["affinity_cpus"])
+    if info.get("cgroup_cpu_quota"):
+        c.append(max(1, int(info["cgroup_cpu_quota"])))
+    return min(c)
+
+
 def cpu_baseline(keys, m, reps=5):
     """The oracle's C restatement (oracle/bloom_oracle.c, -O2) building the same
     C2 filter on T = nproc native threads (bo_build_mt: contiguous key slices,
@@ -86,15 +97,17 @@ def cpu_baseline(keys, m, reps=5):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from bloom_oracle import COracle
     C = COracle()
-    T = os.cpu_count() or 1
+    info = host_cpu_info()
+    T = usable_cpus(info)
     C.build_mt(m, keys[:1_000_000], T)  # warm-up (threads, pages)
     t = _med(lambda: C.build_mt(m, keys, T), reps)
-    quota = host_cpu_info().get("cgroup_cpu_quota")
     return {"value": round(keys.size / t / 1e9, 5), "unit": "Gkeys/s", "cores": T,
-            "kind": "port",
+            "kind": "port", "nproc": info["host_cpus"],
+            "cgroup_cpu_quota": info["cgroup_cpu_quota"],
             "sample": f"full C2 run: {keys.size} keys, m={m}; oracle/bloom_oracle.c -O2 on "
-                      f"{T} native threads (nproc), median of {reps} ({t * 1e3:.1f} ms each)"
-                      + (f"; this process's cgroup CPU quota is {quota} CPUs" if quota else "")}
+                      f"{T} native threads = min(nproc {info['host_cpus']}, affinity "
+                      f"{info['affinity_cpus']}, cgroup quota {info['cgroup_cpu_quota']}), "
+                      f"median of {reps} ({t * 1e3:.1f} ms each)"}
 
 
 def cpu_baseline_detail(keys, m):
@@ -107,7 +120,7 @@ def cpu_baseline_detail(keys, m):
     from bloom_oracle import COracle
     from bloomhip import workloads as W
     import numpy as np
-    T = os.cpu_count() or 1
+    T = usable_cpus(host_cpu_info())
     C0, C2 = COracle("O0"), COracle()
     t_o0 = _med(lambda: C0.build(m, keys), 1)
     t_1 = _med(lambda: C2.build(m, keys), 3)
@@ -135,11 +148,16 @@ def cpu_baseline_detail(keys, m):
     return out
 
 
+# The device code and its dispatch (csrc/Makefile KERNEL_SRCS)
+KERNEL_SOURCES = ("bloom_kernels.hip", "bloom_kernels.h", "bloom_math.h", "bloom_merge.hip",
+                  "bloom_merge.h", "bloom_capi.cpp")
+
+
 def kernel_source_sha():
     """Digest of the kernel sources: a PMC summary counts for the bench line
     only if it was taken from exactly these kernels."""
     h = hashlib.sha256()
-    for name in ("bloom_kernels.hip", "bloom_kernels.h", "bloom_math.h"):
+    for name in KERNEL_SOURCES:
         with open(os.path.join(ROOT, "cs265-lsm-tree_amd", "csrc", name), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
@@ -210,7 +228,41 @@ def prewarm(step_fn, torch, min_s=0.3):
             "source": "sysfs pp_dpm_sclk/pp_dpm_mclk current level, sampled during prewarm"}
 
 
-def probe_c3(torch, bh, steps, warmup):
+LEG_PREWARM_S = 0.3   # untimed, time-based warm-up of every secondary leg
+LEG_MIN_CALLS = 20    # timed calls per secondary leg, whatever --steps is
+
+
+def time_leg(call, torch, prewarm_s=LEG_PREWARM_S, calls=LEG_MIN_CALLS, sync=None):
+    """Wall time per call of a secondary leg: `call` repeated for >= prewarm_s
+    untimed, then `calls` calls timed back to back between two device syncs.
+    Independent of --steps, so the driver's short runs time a warm chip."""
+    sync = sync or torch.cuda.synchronize
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < prewarm_s:
+        call()
+        n += 1
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        call()
+    sync()
+    return (time.perf_counter() - t0) / max(calls, 1), n
+
+
+def load_pins():
+    path = os.path.join(ROOT, "tests", "golden", "pins.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def probe_c3(torch, bh):
+    """configs[2] / SURVEY §8d C3: 16.8M GETs against the five level filters
+    in one call.  Each level's packed hit row is checked against the oracle's
+    SHA-256 pin (tests/golden/pins.json), not only its hit count."""
+    import numpy as np
     from bloomhip import workloads as W
     gets, levels = W.c3()
     filters = []
@@ -222,38 +274,48 @@ def probe_c3(torch, bh, steps, warmup):
     nw = (gets.size + 63) // 64
     dout = torch.empty((len(filters), nw), dtype=torch.int64, device="cuda")
     s = torch.cuda.current_stream()
-    for _ in range(warmup):
-        bh.test_batch(filters, dgets, out=dout, stream=s)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        bh.test_batch(filters, dgets, out=dout, stream=s)
-    torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / steps
+    call = lambda: bh.test_batch(filters, dgets, out=dout, stream=s)  # noqa: E731
+    wall, n_pre = time_leg(call, torch)
+    # per-launch device time: HIP events on the launch stream, separate pass
     f0 = filters[0]
     f0.profile(True)
     f0.profile_reset()
-    for _ in range(steps):
-        bh.test_batch(filters, dgets, out=dout, stream=s)
+    for _ in range(LEG_MIN_CALLS):
+        call()
     torch.cuda.synchronize()
     prof = f0.profile_read()
     f0.profile(False)
     kms = sum(v["ms"] for k, v in prof.items()
-              if k in ("k_probe", "probe_partitioned", "k_probe_lds", "probe_stacked")) / steps
+              if k in ("k_probe", "probe_partitioned", "k_probe_lds", "probe_stacked")) / LEG_MIN_CALLS
     hits = dout.cpu().numpy().view("uint64")
-    import numpy as np
     hit_counts = [int(np.unpackbits(hits[j].view(np.uint8)).sum()) for j in range(len(filters))]
+    pins = load_pins()
+    sha_ok = None
+    if pins:
+        want = {lv["level"]: lv["hits_sha256"] for lv in pins["oracle"]["c3"]["levels"]}
+        got = {lvl: hashlib.sha256(hits[j].tobytes()).hexdigest()
+               for j, (lvl, _, _) in enumerate(levels)}
+        sha_ok = got == want
+        if not sha_ok:
+            log("probe_c3: HIT ROWS DIFFER from the oracle pins")
     algo = 4 * gets.size + sum((m + 63) // 64 * 8 for _, _, m in levels) + len(levels) * nw * 8
+    pmc = pmc_traffic("c3")
+    traffic = None if not pmc or pmc.get("stale") else pmc.get("hbm_bytes_per_probe")
     return {"gkeys_s": round(gets.size / (wall * 1e9), 3),
             "kernel_ms": round(kms, 4), "wall_ms": round(wall * 1e3, 4),
-            "kernels": {k: round(v["ms"] / steps, 4) for k, v in prof.items()},
+            "timed_calls": LEG_MIN_CALLS, "prewarm_calls": n_pre,
+            "kernels": {k: round(v["ms"] / LEG_MIN_CALLS, 4) for k, v in prof.items()},
             "algorithmic_bytes": algo,
             "achieved_GBps": round(algo / (kms * 1e-3) / 1e9, 1),
             "frac": round(algo / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-            "hits_per_level": hit_counts}
+            "traffic": traffic,
+            "traffic_ratio": round(traffic / algo, 2) if traffic else None,
+            "traffic_source": "profiles/pmc_c3.json" if traffic else None,
+            "hits_per_level": hit_counts,
+            "hits_sha_match": sha_ok}
 
 
-def route_c3(torch, bh, steps, warmup):
+def route_c3(torch, bh):
     """§8f row 1: batched GET routing of C3's 16.8M GETs over the five level
     runs (range check + filter probe + newest candidate + page index), all
     outputs device-resident."""
@@ -270,20 +332,15 @@ def route_c3(torch, bh, steps, warmup):
     df = torch.empty(n, dtype=torch.int32, device="cuda")
     dp = torch.empty(n, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
-    for _ in range(warmup):
-        bh.route_gets(runs, dgets, cand=dc, first=df, page=dp, stream=s)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        bh.route_gets(runs, dgets, cand=dc, first=df, page=dp, stream=s)
-    torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / steps
+    wall, n_pre = time_leg(
+        lambda: bh.route_gets(runs, dgets, cand=dc, first=df, page=dp, stream=s), torch)
     routed = int((df >= 0).sum().item())
     return {"gkeys_s": round(n / (wall * 1e9), 3), "wall_ms": round(wall * 1e3, 4),
+            "timed_calls": LEG_MIN_CALLS, "prewarm_calls": n_pre,
             "keys_with_candidate": routed}
 
 
-def probe_c3_sharded(torch, bh, dist, rank, world, steps, warmup, coll_dev):
+def probe_c3_sharded(torch, bh, dist, rank, world, coll_dev):
     """SURVEY §8e's probe side at N > 1: every rank holds the five C3 level
     filters (built locally from the same run keys: replicas, no collective)
     and probes its contiguous slice of the 16.8M GETs (shard.probe_slice).
@@ -302,16 +359,15 @@ def probe_c3_sharded(torch, bh, dist, rank, world, steps, warmup, coll_dev):
     nw = (hi - lo + 63) // 64
     dout = torch.empty((len(filters), max(nw, 1)), dtype=torch.int64, device="cuda")
     s = torch.cuda.current_stream()
-    for _ in range(warmup):
-        bh.test_batch(filters, dg, out=dout, stream=s)
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        bh.test_batch(filters, dg, out=dout, stream=s)
-    torch.cuda.synchronize()
-    dist.barrier()
-    el = shard.max_over_ranks((time.perf_counter() - t0) / steps, dist, device=coll_dev)
+
+    def sync():
+        torch.cuda.synchronize()
+        dist.barrier()
+    call = lambda: bh.test_batch(filters, dg, out=dout, stream=s)  # noqa: E731
+    time_leg(call, torch, calls=0)
+    sync()
+    el, _ = time_leg(call, torch, prewarm_s=0.0, sync=sync)
+    el = shard.max_over_ranks(el, dist, device=coll_dev)
     hits = [int(np.unpackbits(dout[j].cpu().numpy().view(np.uint8)).sum())
             for j in range(len(filters))] if hi > lo else [0] * len(filters)
     tot = [int(shard.sum_over_ranks(h, dist, device=coll_dev)) for h in hits]
@@ -325,7 +381,7 @@ def probe_c3_sharded(torch, bh, dist, rank, world, steps, warmup, coll_dev):
             "note": "filters replicated per GPU, GET keys sharded contiguously, no data collective"}
 
 
-def c5_eight_runs(torch, bh, dist, rank, world, steps, warmup, coll_dev):
+def c5_eight_runs(torch, bh, dist, rank, world, coll_dev):
     """BASELINE configs[4] / SURVEY §8d C5: 8 independent runs r = 0..7 of
     67,108,864 keys (seed 13141 + r, 10 bits/key), run r built on rank
     r % N, one after another on its GPU; no collective on the data path.
@@ -356,18 +412,15 @@ def c5_eight_runs(torch, bh, dist, rank, world, steps, warmup, coll_dev):
         pins = json.load(open(pins_path))["oracle"]["c5"]
     ok = None if pins is None else all(
         hashlib.sha256(f.words().tobytes()).hexdigest() == pins[r]["sha256"] for r, _, f in built)
-    for _ in range(warmup):
-        step()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    el = (time.perf_counter() - t0) / steps
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+    # every rank warms up on its own, then the timed calls start together
+    time_leg(step, torch, calls=0)
+    sync()
+    el, _ = time_leg(step, torch, prewarm_s=0.0, sync=sync)
     if dist:
         from bloomhip import shard
         el = shard.max_over_ranks(el, dist, device=coll_dev)
@@ -380,7 +433,7 @@ def c5_eight_runs(torch, bh, dist, rank, world, steps, warmup, coll_dev):
             "note": "8 runs x 64M keys (configs[4]); run r on rank r % N; rate = all 8 runs / max-rank time"}
 
 
-def compact_fanin(torch, bh, reps):
+def compact_fanin(torch, bh):
     """§8f row 3: a fan-in-4 compaction (4 runs x 4M entries, newest first)
     merged on the device and fused with the new run's filter + fence build
     (bloomhip_compact, synchronous), device-resident in and out."""
@@ -390,19 +443,100 @@ def compact_fanin(torch, bh, reps):
     total = sum(r.shape[0] for r in runs)
     dout = torch.empty((total, 2), dtype=torch.int32, device="cuda")
     f = bh.BloomFilter(m)
-    for _ in range(2):
-        got = bh.compact(druns, drop_tombstones=True, filter=f, out=dout)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
+    got = [None]
+
+    def call():
         f.clear()
-        got = bh.compact(druns, drop_tombstones=True, filter=f, out=dout)
-    torch.cuda.synchronize()
-    t = (time.perf_counter() - t0) / reps
+        got[0] = bh.compact(druns, drop_tombstones=True, filter=f, out=dout)
+    t, n_pre = time_leg(call, torch)
     return {"gentries_s": round(total / t / 1e9, 3), "ms": round(t * 1e3, 3),
-            "entries_in": total, "entries_out": int(got.shape[0]),
+            "timed_calls": LEG_MIN_CALLS, "prewarm_calls": n_pre,
+            "entries_in": total, "entries_out": int(got[0].shape[0]),
             "note": "4 sorted runs merged newest-wins + tombstones dropped + filter/fences "
                     "of the merged run built; wall clock per synchronous call"}
+
+
+def c4_build(torch, bh, reps=LEG_MIN_CALLS):
+    """configs[3] / SURVEY §8d C4: one run of 268,435,456 keys at 12 bits/key
+    (m = 3,221,225,472 bits, a 384 MiB bitmap: beyond LDS, L2 and most of
+    the Infinity Cache).  The bitmap is checked against the oracle's SHA-256
+    pin; the device time per build comes from HIP events on the launch stream
+    around `reps` back-to-back builds (after a time-based prewarm), the
+    roofline from (4N + m/8) per build, traffic from profiles/pmc_c4.json."""
+    from bloomhip import workloads as W
+    keys, m = W.c4()
+    n = keys.size
+    dk = torch.from_numpy(keys).cuda()
+    del keys
+    f = bh.BloomFilter(m)
+    s = torch.cuda.current_stream()
+
+    def step():
+        f.clear(stream=s)
+        f.set_batch(dk, stream=s)
+    step()
+    torch.cuda.synchronize()
+    pins = load_pins()
+    ok = None
+    if pins:
+        ok = hashlib.sha256(f.words().tobytes()).hexdigest() == pins["oracle"]["c4"]["sha256"]
+        if not ok:
+            log("c4_build: BITMAP MISMATCH vs oracle fixture")
+    time_leg(step, torch, calls=0)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(s)
+    for _ in range(reps):
+        step()
+    ev1.record(s)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    dev_ms = ev0.elapsed_time(ev1) / reps
+    f.profile(True)
+    f.profile_reset()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    prof = f.profile_read()
+    f.profile(False)
+    algo = 4 * n + (m + 63) // 64 * 8
+    achieved = algo / (dev_ms * 1e-3) / 1e9
+    pmc = pmc_traffic("c4")
+    traffic = None if not pmc or pmc.get("stale") else pmc.get("hbm_bytes_per_build")
+    out = {"gkeys_s": round(n / (dev_ms * 1e-3) / 1e9, 3), "device_ms": round(dev_ms, 4),
+           "wall_ms": round(wall * 1e3, 4), "builds_timed": reps,
+           "keys": n, "m_bits": m, "strategy": bh.STRATEGY_NAMES[f.resolve_strategy(n)],
+           "kernels": {k: round(v["ms"] / v["launches"], 4) for k, v in prof.items()},
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                        "traffic": traffic,
+                        "traffic_ratio": round(traffic / algo, 2) if traffic else None,
+                        "traffic_source": "profiles/pmc_c4.json" if traffic else None,
+                        "algorithmic_bytes": algo},
+           "verified_vs_oracle": ok}
+    del dk, f
+    bh.lib().bloomhip_trim()  # the 3 GB partition workspace of this size
+    torch.cuda.empty_cache()
+    return out
+
+
+def c1_check(bh):
+    """configs[0] / SURVEY §8d C1: the first flushed run of generator --puts
+    100000 (-b 100 -r 10) as AoS entry_t {key, val} at stride 8, built on the
+    GPU and compared word for word with the oracle's whole bitmap
+    (tests/golden/c1_bitmap.npy)."""
+    import numpy as np
+    from bloomhip import workloads as W
+    run, m = W.c1_run()
+    f = bh.BloomFilter(m)
+    f.set_batch(run.reshape(-1), n=run.shape[0], stride=8)
+    got = f.words()
+    path = os.path.join(ROOT, "tests", "golden", "c1_bitmap.npy")
+    ok = bool((got == np.load(path)).all()) if os.path.exists(path) else None
+    return {"entries": int(run.shape[0]), "m_bits": m, "stride": 8,
+            "strategy": bh.STRATEGY_NAMES[f.resolve_strategy(run.shape[0])],
+            "verified_vs_oracle": ok}
 
 
 def e2e_build(torch, bh, keys_np, m, reps=10):
@@ -501,6 +635,41 @@ def scalar_is_set(bh, f, keys_np, calls=4000):
                     "kernel on the default stream, answer in a pinned mapped host word"}
 
 
+def launch_ranks(n):
+    """bench.py --gpus N without a launcher (no WORLD_SIZE in the environment):
+    start N copies of this command as ranks 0..N-1 of one process group on
+    127.0.0.1, one per GPU (LOCAL_RANK = rank), and wait for them.  This
+    process never touches a GPU (no torch, no bloomhip), so nothing is
+    initialised before the children start.  Returns the first non-zero exit
+    status of a rank (the others are then stopped), else 0."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 1
+                log(f"bench: rank {procs.index(p)} exited with {rc}; stopping the others")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -513,10 +682,22 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 eight-run leg")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed time-based warm-up before --warmup (0 under profilers)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 build leg")
     args = ap.parse_args()
+    if args.gpus < 1:
+        log(f"--gpus must be >= 1 (got {args.gpus})")
+        sys.exit(2)
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # Not started by a launcher: become one (nothing has touched a GPU yet).
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus {args.gpus}: refusing to measure a different "
+            f"number of GPUs than asked for")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import numpy as np
@@ -625,21 +806,24 @@ def main():
     if not args.no_extras and not args.no_c5:
         if rank == 0:
             log("C5 eight runs ...")
-        extras["c5_eight_runs"] = c5_eight_runs(torch, bh, dist, rank, world,
-                                                max(3, args.steps // 20), 1, coll_dev)
+        extras["c5_eight_runs"] = c5_eight_runs(torch, bh, dist, rank, world, coll_dev)
         torch.cuda.empty_cache()
     if world > 1 and not args.no_extras:
         if rank == 0:
             log("sharded probe C3 ...")
-        extras["probe_c3_sharded"] = probe_c3_sharded(torch, bh, dist, rank, world,
-                                                      max(5, args.steps // 5), 2, coll_dev)
+        extras["probe_c3_sharded"] = probe_c3_sharded(torch, bh, dist, rank, world, coll_dev)
     if rank == 0 and world == 1 and not args.no_extras:
+        log("C1 stride-8 run ...")
+        extras["c1_check"] = c1_check(bh)
+        if not args.no_c4:
+            log("C4 build ...")
+            extras["c4_build"] = c4_build(torch, bh)
         log("probe C3 ...")
-        extras["probe_c3"] = probe_c3(torch, bh, max(5, args.steps // 5), 2)
+        extras["probe_c3"] = probe_c3(torch, bh)
         log("route C3 ...")
-        extras["route_c3"] = route_c3(torch, bh, max(5, args.steps // 5), 2)
+        extras["route_c3"] = route_c3(torch, bh)
         log("compact ...")
-        extras["compact_fanin4"] = compact_fanin(torch, bh, max(3, args.steps // 20))
+        extras["compact_fanin4"] = compact_fanin(torch, bh)
         log("e2e ...")
         extras["e2e_build"] = e2e_build(torch, bh, keys, m)
         extras["e2e_probe_c3"] = e2e_probe_c3(torch, bh)
@@ -719,6 +903,15 @@ def main():
         "verified_vs_oracle": all_ok if verified is not None or dist else None,
     }
     line.update(extras)
+    # Every BASELINE config this run exercised, with its oracle check (None:
+    # not run, or no pin for it).
+    line["parity"] = {
+        "c1_stride8_bitmap": (extras.get("c1_check") or {}).get("verified_vs_oracle"),
+        f"{args.workload}_bitmap_sha": line["verified_vs_oracle"],
+        "c3_hits_sha": (extras.get("probe_c3") or {}).get("hits_sha_match"),
+        "c4_bitmap_sha": (extras.get("c4_build") or {}).get("verified_vs_oracle"),
+        "c5_eight_bitmaps_sha": (extras.get("c5_eight_runs") or {}).get("verified_vs_oracle"),
+    }
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -87,6 +87,7 @@ struct SegMap {
     uint32_t magic;
     uint32_t nbins;
     uint32_t scaled_shift;  // shift + l: the same map on a remainder scaled by 2^l (mod_fast_scaled)
+    uint32_t p2_hi_shift;   // t - shift: where (x >> t) % d lands in p >> shift (m = d << t)
 };
 
 struct PartitionWorkspace {
@@ -104,7 +105,7 @@ struct PartitionWorkspace {
 };
 
 inline SegMap seg_map_of(const PartitionWorkspace &ws) {
-    return SegMap{ws.sub_shift - 1, ws.magic, (uint32_t)ws.nbins, 0};
+    return SegMap{ws.sub_shift - 1, ws.magic, (uint32_t)ws.nbins, 0, 0};
 }
 
 // Keys per pass-1 tile for a batch sorted into nbins segments: short runs

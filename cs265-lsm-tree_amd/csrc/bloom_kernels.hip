@@ -45,7 +45,7 @@ __device__ __forceinline__ int32_t load_key(const KeySpan &ks, size_t i) {
 }
 
 __device__ __forceinline__ uint32_t pos32(uint64_t raw, const ModParams &mp) {
-    return mod_fast(raw, mp);
+    return mod_32(raw, mp);
 }
 
 __device__ __forceinline__ void global_or(uint32_t *words, uint64_t p) {
@@ -143,7 +143,12 @@ __global__ void __launch_bounds__(kBlock) k_build_lds(KeySpan ks, ModParams mp,
 // workgroup barriers wait only for LDS (lgkmcnt), so the sorted tile's
 // stores drain under the next tile's hashing.
 //
-// WIDE: m >= 2^32 (64-bit positions, mod_wide); the entries are the same.
+// MK (how a position is reduced mod m): kModFast, the general remainder for
+// m < 2^32 kept scaled by 2^l; kModWide, m >= 2^32 (64-bit positions,
+// mod_wide; the entries are the same); kModP2, m = d << t with d | 255 and
+// t >= kEntryBits (bloom_math.h mod_p2_hi): the entry is the key hash's own
+// low 21 bits and p >> shift = (x >> t) % d << (t - shift) | bits shift..t-1
+// of x, so only the 5-instruction (x >> t) % d is left of the remainder.
 // SLOTS (partitioned probe): also write, per key and hash, the index its
 // position got in the sorted tile: slots[(tile*3 + h)*tile_keys + key].
 // ---------------------------------------------------------------------------
@@ -258,7 +263,9 @@ constexpr uint32_t kBinShift = 19;  // 8192 segments << 19 < 2^32
 // (b = 0..nbins): COLS = true: straight into the segment-major table
 // runs[b * ntiles + tile]; COLS = false: into the tile-major
 // runs[tile * (nbins + 1) + b], for k_runs_transpose (large tables).
-template <int LAYOUT, bool SLOTS, bool COLS, int TB, bool WIDE, int MAXB = 0, int MINW = 4>
+constexpr int kModFast = 0, kModWide = 1, kModP2 = 2;
+
+template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4>
 __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                                                        uint64_t *__restrict__ pos_out,
                                                        uint32_t *__restrict__ runs, SegMap sm,
@@ -307,10 +314,17 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                 for (int h = 0; h < 3; h++) {
                     const uint64_t raw = h == 0 ? raw_hash1(k) : h == 1 ? raw_hash2(k) : raw_hash3(k);
                     uint32_t b;
-                    if constexpr (WIDE) {
+                    if constexpr (MK == kModWide) {
                         const uint64_t p = mod_wide(raw, mp);
                         b = seg_of(p, sm);
                         ent[3 * j + h] = (uint32_t)p & kEntryMask;
+                    } else if constexpr (MK == kModP2) {
+                        const uint32_t xl = (uint32_t)raw;
+                        const uint32_t r = mod_p2_hi(raw, mp);
+                        const uint32_t q = (r << sm.p2_hi_shift) |
+                                           __builtin_amdgcn_ubfe(xl, sm.shift, sm.p2_hi_shift);
+                        b = __umulhi(q, sm.magic);
+                        ent[3 * j + h] = xl & kEntryMask;
                     } else {
                         // the remainder still scaled by 2^l: the entry is a
                         // bit-field of it, and one shift reaches the segment
@@ -826,7 +840,7 @@ __global__ void __launch_bounds__(kBlock) k_probe(KeySpan ks, ProbeTable t,
 // the reference's && result.
 constexpr int kProbeLdsBlock = 1024;
 
-template <int LAYOUT>
+template <int LAYOUT, bool P2>
 __global__ void __launch_bounds__(kProbeLdsBlock) k_probe_lds(KeySpan ks, const uint32_t *words,
                                                              ModParams mp, uint32_t nw32,
                                                              uint64_t *__restrict__ out,
@@ -847,9 +861,9 @@ __global__ void __launch_bounds__(kProbeLdsBlock) k_probe_lds(KeySpan ks, const 
             if constexpr (LAYOUT == KEYS_PACKED) k = reinterpret_cast<const int32_t *>(ks.base)[i];
             else k = load_key<LAYOUT>(ks, i);
         }
-        const uint32_t p1 = mod_fast(raw_hash1(k), mp);
-        const uint32_t p2 = mod_fast(raw_hash2(k), mp);
-        const uint32_t p3 = mod_fast(raw_hash3(k), mp);
+        const uint32_t p1 = P2 ? mod_p2(raw_hash1(k), mp) : mod_fast(raw_hash1(k), mp);
+        const uint32_t p2 = P2 ? mod_p2(raw_hash2(k), mp) : mod_fast(raw_hash2(k), mp);
+        const uint32_t p3 = P2 ? mod_p2(raw_hash3(k), mp) : mod_fast(raw_hash3(k), mp);
         const uint32_t hit = (filt[p1 >> 5] >> (p1 & 31)) & (filt[p2 >> 5] >> (p2 & 31)) &
                              (filt[p3 >> 5] >> (p3 & 31)) & 1u;
         const uint64_t ballot = __ballot(valid && hit);
@@ -1365,32 +1379,39 @@ bool runs_as_columns(const PartitionWorkspace &ws) {
 // C2's 256 segments at MAXB 511 run pass 1 in 74.5 us against 87 at 4096,
 // tools/ubench.py part with UB_P1).  Only the packed / entry_t fast paths get
 // the small capacities; strided keys and m >= 2^32 use the largest.
-template <int L, bool SLOTS, int TB, bool W, int MAXB>
+template <int L, bool SLOTS, int TB, int MK, int MAXB>
 void bin_launch(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                 uint32_t *runs, const SegMap &sm, bool cols, unsigned grid, uint16_t *slots,
                 hipStream_t stream) {
     if (cols)
-        k_part_bin<L, SLOTS, true, TB, W, MAXB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm,
-                                                                        ws.ntiles, slots);
-    else
-        k_part_bin<L, SLOTS, false, TB, W, MAXB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm,
+        k_part_bin<L, SLOTS, true, TB, MK, MAXB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm,
                                                                          ws.ntiles, slots);
+    else
+        k_part_bin<L, SLOTS, false, TB, MK, MAXB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm,
+                                                                          ws.ntiles, slots);
 }
 
-template <int L, bool SLOTS, int TB>
+template <int L, bool SLOTS, int TB, int MK>
 void bin_launch_fast(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                      uint32_t *runs, const SegMap &sm, bool cols, unsigned grid, uint16_t *slots,
                      hipStream_t stream) {
     const size_t nb = ws.nbins;
     if constexpr (TB >= 1024) {
-        if (nb <= 1023) bin_launch<L, SLOTS, TB, false, 1023>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
-        else if (nb <= 2047) bin_launch<L, SLOTS, TB, false, 2047>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
-        else if (nb <= 4095) bin_launch<L, SLOTS, TB, false, 4095>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
-        else bin_launch<L, SLOTS, TB, false, (int)kPartMaxBinsBig>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        if (nb <= 1023) bin_launch<L, SLOTS, TB, MK, 1023>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else if (nb <= 2047) bin_launch<L, SLOTS, TB, MK, 2047>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else if (nb <= 4095) bin_launch<L, SLOTS, TB, MK, 4095>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else bin_launch<L, SLOTS, TB, MK, (int)kPartMaxBinsBig>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
     } else {
-        if (nb <= 511) bin_launch<L, SLOTS, TB, false, 511>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
-        else bin_launch<L, SLOTS, TB, false, (int)kPartMaxBins>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        if (nb <= 511) bin_launch<L, SLOTS, TB, MK, 511>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else bin_launch<L, SLOTS, TB, MK, (int)kPartMaxBins>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
     }
+}
+
+// Whether pass 1 may take the p2 reduction (kModP2) for this geometry: the
+// entry must be the hash's low kEntryBits bits (t >= 21) and p >> shift must
+// reach bit t (shift <= t).
+inline bool p2_pass1(const ModParams &mp, const SegMap &sm) {
+    return mp.fast && mp.p2 && mp.p2t >= kEntryBits && sm.shift <= mp.p2t && mp.p2t - sm.shift < 32;
 }
 
 template <bool SLOTS, int TB>
@@ -1410,22 +1431,31 @@ hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const Partition
             sm.magic = 0;
         }
     }
+    const bool p2 = p2_pass1(mp, sm);
+    if (p2) sm.p2_hi_shift = mp.p2t - sm.shift;
     const bool entry16 =
         ks.layout == KEYS_ENTRY && (reinterpret_cast<uintptr_t>(ks.base) & 15) == 0;
     if (wide) {
         if (ks.layout == KEYS_PACKED)
-            bin_launch<KEYS_PACKED, SLOTS, TB, true, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch<KEYS_PACKED, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
         else if (entry16)
-            bin_launch<KEYS_ENTRY, SLOTS, TB, true, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch<KEYS_ENTRY, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
         else
-            bin_launch<KEYS_STRIDED, SLOTS, TB, true, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch<KEYS_STRIDED, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+    } else if (p2) {
+        if (ks.layout == KEYS_PACKED)
+            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModP2>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else if (entry16)
+            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModP2>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        else
+            bin_launch<KEYS_STRIDED, SLOTS, TB, kModP2, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
     } else {
         if (ks.layout == KEYS_PACKED)
-            bin_launch_fast<KEYS_PACKED, SLOTS, TB>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModFast>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
         else if (entry16)
-            bin_launch_fast<KEYS_ENTRY, SLOTS, TB>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModFast>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
         else
-            bin_launch<KEYS_STRIDED, SLOTS, TB, false, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch<KEYS_STRIDED, SLOTS, TB, kModFast, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess || cols) return e;
@@ -1579,10 +1609,12 @@ hipError_t launch_probe_lds(const KeySpan &ks, const ModParams &mp, const uint32
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
     if (!mp.fast || nw32 * 4 > kLdsBitmapBytes) return hipErrorInvalidValue;
     static const bool attr_set = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_probe_lds<KEYS_PACKED>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBitmapBytes);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_probe_lds<KEYS_STRIDED>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBitmapBytes);
+        for (const void *fn : {reinterpret_cast<const void *>(&k_probe_lds<KEYS_PACKED, false>),
+                               reinterpret_cast<const void *>(&k_probe_lds<KEYS_STRIDED, false>),
+                               reinterpret_cast<const void *>(&k_probe_lds<KEYS_PACKED, true>),
+                               reinterpret_cast<const void *>(&k_probe_lds<KEYS_STRIDED, true>)})
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kLdsBitmapBytes);
         return true;
     }();
     (void)attr_set;
@@ -1592,12 +1624,15 @@ hipError_t launch_probe_lds(const KeySpan &ks, const ModParams &mp, const uint32
     const unsigned per_cu = lds * 2 <= kLdsBitmapBytes ? 2u : 1u;
     const unsigned grid =
         grid_for(nw_out, 64 * (kProbeLdsBlock / 64), per_cu * (unsigned)device_cu_count());
-    if (ks.layout == KEYS_PACKED)
-        k_probe_lds<KEYS_PACKED><<<grid, kProbeLdsBlock, lds, stream>>>(ks, words, mp,
-                                                                       (uint32_t)nw32, out, nw_out);
-    else
-        k_probe_lds<KEYS_STRIDED><<<grid, kProbeLdsBlock, lds, stream>>>(
-            ks, words, mp, (uint32_t)nw32, out, nw_out);
+#define PROBE_LDS(L, P)                                                                  \
+    k_probe_lds<L, P><<<grid, kProbeLdsBlock, lds, stream>>>(ks, words, mp, (uint32_t)nw32, \
+                                                             out, nw_out)
+    if (ks.layout == KEYS_PACKED) {
+        if (mp.p2) PROBE_LDS(KEYS_PACKED, true); else PROBE_LDS(KEYS_PACKED, false);
+    } else {
+        if (mp.p2) PROBE_LDS(KEYS_STRIDED, true); else PROBE_LDS(KEYS_STRIDED, false);
+    }
+#undef PROBE_LDS
     return hipGetLastError();
 }
 

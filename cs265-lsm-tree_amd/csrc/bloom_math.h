@@ -121,9 +121,27 @@ struct ModParams {
     uint32_t v;   // floor((2^64-1)/dn) - 2^32       (fast path)
     uint32_t l;   // leading zeros of m as a u32     (fast path)
     uint32_t fast;  // 1 when m <= 0xFFFFFFFF
-    uint32_t pad;
+    uint32_t p2;    // 1 when m = d << t with d | 255, d >= 3, 12 <= t < 32 (p2 path)
     double minv;  // 1.0 / m                         (wide path)
+    uint32_t p2t;   // t                             (p2 path)
+    uint32_t p2d;   // d
+    uint32_t p2M;   // ceil(2^32 / d)
+    uint32_t p2pad;
 };
+
+// m = d << t with d | 255 (d in 3, 5, 15, 17, 51, 85, 255) and 12 <= t < 32:
+// the form every LSM filter of the reference's configs takes (Run::Run sizes
+// m = capacity * bits/entry, a power-of-two page count times 5 at 10 bits per
+// entry, times 3 at 12: C2 5<<25, C3 5<<(17+2i), C4 3<<30, C5 5<<27).
+inline bool p2_form(uint64_t m, uint32_t *d_out, uint32_t *t_out) {
+    if (m == 0 || m > 0xFFFFFFFFull) return false;
+    uint32_t t = (uint32_t)__builtin_ctzll(m);
+    const uint64_t d = m >> t;
+    if (t < 12 || t >= 32 || d < 3 || 255 % d != 0) return false;
+    *d_out = (uint32_t)d;
+    *t_out = t;
+    return true;
+}
 
 // Host-side precomputation (m >= 1).
 inline ModParams make_mod_params(uint64_t m) {
@@ -138,9 +156,49 @@ inline ModParams make_mod_params(uint64_t m) {
         p.dn = dn;
         p.v = (uint32_t)(~0ull / dn - (1ull << 32));
         p.R = (uint32_t)((1ull << 32) % m);
+        uint32_t d = 0, t = 0;
+        if (p2_form(m, &d, &t)) {
+            p.p2 = 1;
+            p.p2t = t;
+            p.p2d = d;
+            p.p2M = (uint32_t)(((1ull << 32) + d - 1) / d);
+        }
     }
     p.minv = m ? 1.0 / (double)m : 0.0;
     return p;
+}
+
+// (x >> t) % d for m = d << t (p.p2).  d | 255 makes 2^8 = 1 (mod d), so a
+// number is congruent mod d to the sum of its bytes: y = x >> t is
+// yh * 2^32 + yl with yh = xh >> t < 2^20, and
+//   y = yh + (sum of yl's four bytes)   (mod d),
+// a sum s < 2^21 that gfx950 forms in ONE v_sad_u8 (|yl.b_i - 0| summed,
+// plus yh).  Then q = mulhi(s, M) with M = ceil(2^32/d) = (2^32 + e)/d,
+// e < d, is floor(s/d) exactly: s*M/2^32 = s/d + s*e/(d*2^32), and the excess
+// stays below the 1/d gap to the next integer because s*e < 2^21 * 255 < 2^32.
+// r = s - q*d is one v_mad_i32_i24 (q < 2^20, d < 2^8).
+// 5 instructions (alignbit, shift, sad, mulhi, mad) against the general
+// remainder's 10; tests/test_host.py fuzzes it against the oracle.
+BH_HD uint32_t mod_p2_hi(uint64_t x, const ModParams &p) {
+    const uint32_t xh = (uint32_t)(x >> 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t yl = __builtin_amdgcn_alignbit(xh, (uint32_t)x, p.p2t);
+    const uint32_t s = __builtin_amdgcn_sad_u8(yl, 0u, xh >> p.p2t);
+    const uint32_t q = __umulhi(s, p.p2M);
+    return (uint32_t)((int)s + __mul24((int)q, -(int)p.p2d));  // one v_mad_i32_i24
+#else
+    const uint32_t yl = (uint32_t)(x >> p.p2t);
+    const uint32_t s = (yl & 0xFFu) + ((yl >> 8) & 0xFFu) + ((yl >> 16) & 0xFFu) + (yl >> 24) +
+                       (xh >> p.p2t);
+    const uint32_t q = (uint32_t)(((uint64_t)s * p.p2M) >> 32);
+    return s - q * p.p2d;
+#endif
+}
+
+// x % m for m = d << t (p.p2): ((x >> t) % d) << t | (x mod 2^t).
+BH_HD uint32_t mod_p2(uint64_t x, const ModParams &p) {
+    const uint32_t r = mod_p2_hi(x, p);
+    return (r << p.p2t) | ((uint32_t)x & ((1u << p.p2t) - 1u));
 }
 
 // (x % m) << l for m < 2^32 (p.fast): the remainder before the final
@@ -177,8 +235,13 @@ BH_HD uint64_t mod_wide(uint64_t x, const ModParams &p) {
     return r;
 }
 
+// x % m for m < 2^32: the p2 form when m has it, else the general remainder.
+BH_HD uint32_t mod_32(uint64_t x, const ModParams &p) {
+    return p.p2 ? mod_p2(x, p) : mod_fast(x, p);
+}
+
 BH_HD uint64_t mod_any(uint64_t x, const ModParams &p) {
-    return p.fast ? (uint64_t)mod_fast(x, p) : mod_wide(x, p);
+    return p.fast ? (uint64_t)mod_32(x, p) : mod_wide(x, p);
 }
 
 // ---- exact q = x / S for 32-bit x, runtime S >= 2 (Granlund–Montgomery,

@@ -231,7 +231,7 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
         SegMap sm = seg_map_of(ws);                                                              \
         sm.scaled_shift = sm.shift + mp.l;                                                       \
         const unsigned g = (unsigned)std::min<size_t>(ws.ntiles, (size_t)device_cu_count() * NWG); \
-        k_part_bin<KEYS_PACKED, false, true, TB, false, MAXB, MINW>                              \
+        k_part_bin<KEYS_PACKED, false, true, TB, kModFast, MAXB, MINW>                              \
             <<<g, TB, 0, s>>>(ks, mp, ws.pos, RUNS, sm, ws.ntiles, nullptr);            \
         e = hipGetLastError();                                                                   \
         break;                                                                                   \

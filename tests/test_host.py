@@ -198,6 +198,26 @@ def test_binding_refuses_keys_that_are_not_int32():
         bh.compact([np.zeros((4, 2), dtype=np.int64)])
 
 
+P2_D = (3, 5, 15, 17, 51, 85, 255)
+
+
+def test_engine_p2_mod_every_form(fuzz_keys):
+    """The p2 remainder (bloom_math.h mod_p2: m = d << t with d | 255, the
+    byte-sum congruence and one multiply-high) against the exact remainder
+    for every d and t it takes, and the m either side of each (general path)."""
+    checked = 0
+    for d in P2_D:
+        for t in range(12, 32):
+            m = d << t
+            if m >= 2**32:
+                continue
+            for mm in (m, m - 1, m + 1):
+                assert (bh.host_positions(mm, fuzz_keys[:4000]) ==
+                        np_positions(fuzz_keys[:4000], mm)).all(), (d, t, mm)
+            checked += 1
+    assert checked > 100
+
+
 def test_engine_wide_mod_random_m(fuzz_keys):
     """mod_wide (2^32 <= m <= 2^46: double-estimated quotient + one exact
     correction) against the exact remainder, m spread over the whole range
@@ -223,7 +243,26 @@ def test_library_is_built_from_these_kernel_sources():
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     h = hashlib.sha256()
-    for name in ("bloom_kernels.hip", "bloom_kernels.h", "bloom_math.h"):
+    for name in KERNEL_SOURCES:
         with open(os.path.join(root, "cs265-lsm-tree_amd", "csrc", name), "rb") as f:
             h.update(f.read())
     assert bh.lib().bloomhip_kernel_sha().decode() == h.hexdigest()[:16]
+
+
+# every source the device code and its dispatch are built from (the digest
+# compiled into the library; csrc/Makefile KERNEL_SRCS, bench.KERNEL_SOURCES)
+KERNEL_SOURCES = ("bloom_kernels.hip", "bloom_kernels.h", "bloom_math.h", "bloom_merge.hip",
+                  "bloom_merge.h", "bloom_capi.cpp")
+
+
+def test_digest_lists_agree():
+    import os
+    import re
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mk = open(os.path.join(root, "cs265-lsm-tree_amd", "csrc", "Makefile")).read()
+    srcs = re.search(r"^KERNEL_SRCS\s*:?=\s*(.+)$", mk, re.M).group(1).split()
+    assert tuple(srcs) == KERNEL_SOURCES
+    sys.path.insert(0, root)
+    import bench
+    assert tuple(bench.KERNEL_SOURCES) == KERNEL_SOURCES

@@ -45,6 +45,10 @@ for s in ${STEPS//,/ }; do
             pmc c2 WRITE_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
     pmc_c4) pmc c4 FETCH_SIZE --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
             pmc c4 WRITE_SIZE --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
+    pmc_c3) run pmc_c3_FETCH_SIZE 150 timeout -s KILL 140 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_c3_FETCH_SIZE" -o pmc --output-format csv -- python tools/probe_prof.py auto 10 || exit 1
+            run pmc_c3_WRITE_SIZE 150 timeout -s KILL 140 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_c3_WRITE_SIZE" -o pmc --output-format csv -- python tools/probe_prof.py auto 10 || exit 1 ;;
+    bench_dist2) run bench_dist2 600 env BLOOMHIP_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline || exit 1 ;;
+    bench_driver) run bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
     pmc_c5) pmc c5 FETCH_SIZE --workload c5 --steps 5 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
             pmc c5 WRITE_SIZE --workload c5 --steps 5 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -6,6 +6,7 @@ correction of MI355X_MICROARCH.md, HBM section: it tallies 128-B requests at
 workload's own build; smaller grids are the tests' warm-up builds).
 
 Usage: pmc_traffic.py WORKLOAD TAG  -> profiles/pmc_WORKLOAD.json
+(WORKLOAD c3: the C3 probe's kernels, tools/probe_prof.py; hbm_bytes_per_probe)
 (TAG = the tools/gpu_steps.sh tag whose pmc_W step wrote gpurun_out/TAG/pmc_W_*)
 """
 import json
@@ -18,6 +19,31 @@ import pmc_summary  # noqa: E402
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD_KERNELS = ("k_part_bin", "k_runs_transpose", "k_part_apply", "k_build_lds",
                  "k_build_atomic")
+
+
+PROBE_KERNELS = ("k_part_bin", "k_runs_transpose", "k_part_apply", "k_probe_combine",
+                 "k_probe_lds", "k_probe")
+
+
+def per_kernel_probe(d):
+    """The C3 probe's kernels (tools/probe_prof.py): pass 1 with slots, the
+    stacked / partitioned pass 2, the combine (and any per-filter probe),
+    each at its largest grid."""
+    best = {}
+    for key, ctrs in pmc_summary.main(d).items():
+        name, grid = key.rsplit(" grid=", 1)
+        base = name.split("<")[0]
+        if base not in PROBE_KERNELS:
+            continue
+        if base == "k_part_apply" and name.startswith("k_part_apply<0"):  # a build's pass 2
+            continue
+        if base == "k_part_bin":
+            targs = [a.strip() for a in name.split("<", 1)[1].split(">")[0].split(",")]
+            if len(targs) > 1 and targs[1] != "true":
+                continue  # the level builds' pass 1
+        if base not in best or int(grid) > best[base][0]:
+            best[base] = (int(grid), name, ctrs)
+    return best
 
 
 def per_kernel(d):
@@ -39,11 +65,13 @@ def per_kernel(d):
 
 
 def main(w, tag):
-    f = per_kernel(os.path.join(ROOT, "gpurun_out", tag, f"pmc_{w}_FETCH_SIZE"))
-    wr = per_kernel(os.path.join(ROOT, "gpurun_out", tag, f"pmc_{w}_WRITE_SIZE"))
+    probe = w == "c3"
+    pk = per_kernel_probe if probe else per_kernel
+    f = pk(os.path.join(ROOT, "gpurun_out", tag, f"pmc_{w}_FETCH_SIZE"))
+    wr = pk(os.path.join(ROOT, "gpurun_out", tag, f"pmc_{w}_WRITE_SIZE"))
     kernels = {}
     total = 0
-    for base in BUILD_KERNELS:
+    for base in (PROBE_KERNELS if probe else BUILD_KERNELS):
         if base not in f or base not in wr:
             continue
         fetch = 2 * f[base][2]["FETCH_SIZE"] * 1024
@@ -55,7 +83,9 @@ def main(w, tag):
         sys.exit(f"pmc_traffic: no build kernels in gpurun_out/{tag}/pmc_{w}_*; nothing written")
     sys.path.insert(0, ROOT)
     from bench import library_kernel_sha as kernel_source_sha
-    out = {"workload": w, "round": tag, "hbm_bytes_per_build": int(total), "kernels": kernels,
+    out = {"workload": w, "round": tag,
+           ("hbm_bytes_per_probe" if probe else "hbm_bytes_per_build"): int(total),
+           "kernels": kernels,
            "kernel_source_sha": kernel_source_sha(),
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
                      "(tools/gpu_steps.sh pmc_W); FETCH_SIZE x2 (gfx950); KiB -> bytes; median per "
