@@ -179,9 +179,13 @@ hipError_t grow_touched(void **ptr, size_t *have, size_t need, hipStream_t s) {
 // Scratch of the partition build / partitioned probe.  Shared by every handle
 // that runs on the same (device, stream): work on one stream is ordered, so
 // one set of buffers serves all of it, allocated (and first touched) once.
-// Lock order everywhere: filter handle(s) first, then the workspace.  The
-// workspace lock is recursive: a compaction holds it across the build of its
-// output run's filter, which takes it again (run_partition).
+// Lock order everywhere: filter handle(s) first, then a workspace; g_ws_mu
+// (the map) is only ever held alone (workspace_for, bloomhip_trim), never
+// while a workspace lock is taken, so a compaction that holds its workspace
+// across the build of its output run's filter cannot deadlock with trim.  The
+// workspace lock is recursive: that build takes it again (run_partition).
+// Callers hold a shared_ptr, so a workspace that bloomhip_trim drops from
+// the map stays alive until its last user is done with it.
 struct Workspace {
     std::recursive_mutex mu;  // held while work using the buffers is enqueued
     uint64_t *pos = nullptr;  // tile-sorted packed entries
@@ -203,13 +207,28 @@ struct Workspace {
 };
 
 std::mutex g_ws_mu;
-std::map<std::pair<int, hipStream_t>, std::unique_ptr<Workspace>> g_ws;
+std::map<std::pair<int, hipStream_t>, std::shared_ptr<Workspace>> g_ws;
 
-Workspace *workspace_for(int device, hipStream_t s) {
+std::shared_ptr<Workspace> workspace_for(int device, hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_ws_mu);
     auto &w = g_ws[{device, s}];
-    if (!w) w.reset(new Workspace());
-    return w.get();
+    if (!w) w = std::make_shared<Workspace>();
+    return w;
+}
+
+// Frees a workspace's buffers (its lock held by the caller; the stream's
+// queued work that uses them is waited for first).
+void free_workspace_buffers(int device, hipStream_t s, Workspace *w) {
+    DeviceGuard g(device);
+    (void)hipStreamSynchronize(s);
+    for (void **p : {(void **)&w->pos, (void **)&w->runs, (void **)&w->res, (void **)&w->slots,
+                     &w->mbuf[0], &w->mbuf[1], (void **)&w->msplit, (void **)&w->mcount,
+                     (void **)&w->mkeys}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    w->pos_bytes = w->runs_bytes = w->res_bytes = w->slots_bytes = 0;
+    w->mbuf_bytes[0] = w->mbuf_bytes[1] = w->msplit_bytes = w->mcount_bytes = w->mkeys_bytes = 0;
 }
 
 hipEvent_t take_event(bloomhip_filter *f) {
@@ -382,10 +401,10 @@ int materialize_clear(bloomhip_filter *f, hipStream_t s) {
 }
 
 int run_partition(bloomhip_filter *f, const KeySpan &ks, hipStream_t s) {
-    Workspace *w = workspace_for(f->device, s);
+    const std::shared_ptr<Workspace> w = workspace_for(f->device, s);
     std::lock_guard<std::recursive_mutex> lk(w->mu);
     PartitionWorkspace ws{};
-    int rc = partition_workspace(w, f->m, ks.n, s, &ws);
+    int rc = partition_workspace(w.get(), f->m, ks.n, s, &ws);
     if (rc) return rc;
     hipError_t e = timed(f, SLOT_PART_BIN, s, [&] { return launch_part_bin(ks, f->mp, ws, s); });
     if (e != hipSuccess) return fail_hip(e, "k_part_bin");
@@ -755,11 +774,11 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
             st.mwords[k] = (uint32_t)(filters[mem[k]]->m / 32);
             st.row[k] = mem[k];
         }
-        Workspace *w = workspace_for(f0->device, s);
+        const std::shared_ptr<Workspace> w = workspace_for(f0->device, s);
         std::lock_guard<std::recursive_mutex> wl(w->mu);
-        int rc = partition_buffers(w, n, s, &ws);
+        int rc = partition_buffers(w.get(), n, s, &ws);
         if (rc) return rc;
-        rc = probe_buffers(w, ws, s);
+        rc = probe_buffers(w.get(), ws, s);
         if (rc) return rc;
         hipError_t e = timed(f0, SLOT_PROBE_STACK, s, [&] {
             return launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s);
@@ -797,12 +816,12 @@ int probe_rows(bloomhip_filter *f0, const bloomhip_filter *const *filters, int n
             if (e != hipSuccess) return fail_hip(e, "k_probe_lds launch");
             continue;
         }
-        Workspace *w = workspace_for(f0->device, s);
+        const std::shared_ptr<Workspace> w = workspace_for(f0->device, s);
         std::lock_guard<std::recursive_mutex> wl(w->mu);
         PartitionWorkspace ws{};
-        rc = partition_workspace(w, filters[j]->m, n, s, &ws);
+        rc = partition_workspace(w.get(), filters[j]->m, n, s, &ws);
         if (rc) return rc;
-        rc = probe_buffers(w, ws, s);
+        rc = probe_buffers(w.get(), ws, s);
         if (rc) return rc;
         hipError_t e = timed(f0, SLOT_PROBE_PART, s, [&] {
             return launch_probe_partitioned(ks, filters[j]->mp, filters[j]->d_words, ws, w->res,
@@ -1127,18 +1146,20 @@ int bloomhip_profile_reset(bloomhip_filter *f) {
 
 int bloomhip_trim(void) {
     g_last_error.clear();
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    for (auto &kv : g_ws) {
+    // Take the map's entries out under g_ws_mu alone, then free each
+    // workspace's buffers under its own lock (the global lock order: never
+    // a workspace lock inside g_ws_mu).  A call that already holds one of
+    // them finishes first; one that starts later gets a fresh workspace.
+    std::map<std::pair<int, hipStream_t>, std::shared_ptr<Workspace>> taken;
+    {
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        taken.swap(g_ws);
+    }
+    for (auto &kv : taken) {
         Workspace *w = kv.second.get();
         std::lock_guard<std::recursive_mutex> wl(w->mu);
-        DeviceGuard g(kv.first.first);
-        (void)hipStreamSynchronize(kv.first.second);
-        for (void *p : {(void *)w->pos, (void *)w->runs, (void *)w->res, (void *)w->slots,
-                        w->mbuf[0], w->mbuf[1], (void *)w->msplit, (void *)w->mcount,
-                        (void *)w->mkeys})
-            if (p) (void)hipFree(p);
+        free_workspace_buffers(kv.first.first, kv.first.second, w);
     }
-    g_ws.clear();
     return BLOOMHIP_OK;
 }
 
@@ -1167,7 +1188,7 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
         // then (filter first, then workspace: the global lock order).
         std::unique_lock<std::mutex> flk;
         if (f) flk = std::unique_lock<std::mutex>(f->mu);
-        Workspace *w = workspace_for(device, s);
+        const std::shared_ptr<Workspace> w = workspace_for(device, s);
         std::lock_guard<std::recursive_mutex> wl(w->mu);
         // + one entry of padding per run: merge outputs start 16-B aligned
         const size_t bytes = (std::max<uint64_t>(total, 1) + (uint64_t)nruns + 2) * 8;

@@ -298,6 +298,7 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
         const size_t tile0 = tile * kTileKeys;
         const int tile_keys = FULL ? (int)kTileKeys : (int)min((size_t)kTileKeys, ks.n - tile0);
         auto live = [&](int j) { return FULL || kPartKPT * tid + j < tile_keys; };
+#pragma clang loop unroll(disable) vectorize(disable)
         for (int b = tid; b <= nb; b += TB) s_hist[b] = (uint32_t)b << kBinShift;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
 
@@ -368,22 +369,16 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                 if (q < per && b <= nb) {
                     // biased by -(b << kBinShift): bin + rank value = byte slot
                     s_hist[b] = run - ((uint32_t)b << kBinShift);
+                    // where segment b's run starts (entry index), straight
+                    // from the scan's registers: segment-major column or
+                    // tile-major row
+                    if constexpr (COLS) runs[(size_t)b * ntiles + tile] = run >> 2;
+                    else runs[tile * (size_t)(nb + 1) + b] = run >> 2;
                     run += local[q];
                 }
             }
         }
         lds_barrier();
-        if constexpr (COLS) {
-            // one bin per thread at C2: a plain loop (the vectorised form the
-            // compiler picked by default costs its setup on every tile)
-            uint32_t *col = runs + (size_t)tid * ntiles + tile;
-#pragma clang loop unroll(disable) vectorize(disable)
-            for (int b = tid; b <= nb; b += TB, col += (size_t)TB * ntiles)
-                *col = (s_hist[b] + ((uint32_t)b << kBinShift)) >> 2;
-        } else {
-            uint32_t *row = runs + tile * (size_t)(nb + 1);
-            for (int b = tid; b <= nb; b += TB) row[b] = (s_hist[b] + ((uint32_t)b << kBinShift)) >> 2;
-        }
         if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
 
         // 3. scatter into the LDS image sorted by segment, one hash at a time:
@@ -424,7 +419,6 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
             }
         }
         lds_barrier();
-
         // 4. the sorted tile goes out packed, three entries per u64, as 16-B
         //    stores: thread t packs entries 6v .. 6v+5 for its vectors v.  In
         //    a short tile the entries past its end are stale, masked so they
@@ -1190,13 +1184,6 @@ __global__ void __launch_bounds__(64) k_is_set1(const uint32_t *__restrict__ wor
            (words[p3 >> 5] >> (p3 & 31)) & 1u;
 }
 
-// Persistent pass-1 grid: two 64-KiB-LDS workgroups per CU for 4096-key
-// tiles, one 112-KiB workgroup for 8192-key tiles.
-inline unsigned part_bin_grid(size_t ntiles, int tb = kPartBlock) {
-    const size_t g = (size_t)device_cu_count() * (tb >= 1024 ? 1 : 2);
-    return (unsigned)(ntiles < g ? ntiles : g);
-}
-
 inline unsigned grid_for(size_t work_items, unsigned per_block, unsigned cap) {
     size_t g = (work_items + per_block - 1) / per_block;
     if (g == 0) g = 1;
@@ -1379,31 +1366,44 @@ bool runs_as_columns(const PartitionWorkspace &ws) {
 // C2's 256 segments at MAXB 511 run pass 1 in 74.5 us against 87 at 4096,
 // tools/ubench.py part with UB_P1).  Only the packed / entry_t fast paths get
 // the small capacities; strided keys and m >= 2^32 use the largest.
+// Workgroups of pass 1 resident per CU: the 4096-key build tile with a
+// histogram of <= 511 bins takes 50 KiB of LDS, so three fit a CU when the
+// registers are capped for 6 waves per SIMD (80 VGPRs, 2 spilled): C2 pass 1
+// 59.5 -> 58.1 us (tools/ubench.py p1ab, variant 5003).  Everything else:
+// two 512-thread or one 1024-thread workgroup per CU.
+template <int TB, bool SLOTS, int MAXB>
+constexpr int part_bin_wgs_per_cu() {
+    return TB >= 1024 ? 1 : (!SLOTS && MAXB > 0 && MAXB <= 511) ? 3 : 2;
+}
+
 template <int L, bool SLOTS, int TB, int MK, int MAXB>
 void bin_launch(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
-                uint32_t *runs, const SegMap &sm, bool cols, unsigned grid, uint16_t *slots,
-                hipStream_t stream) {
+                uint32_t *runs, const SegMap &sm, bool cols, uint16_t *slots, hipStream_t stream) {
+    constexpr int kWgs = part_bin_wgs_per_cu<TB, SLOTS, MAXB>();
+    constexpr int kMinW = kWgs * TB / 256;  // waves per SIMD the registers must allow
+    const size_t g = (size_t)device_cu_count() * kWgs;
+    const unsigned grid = (unsigned)(ws.ntiles < g ? ws.ntiles : g);
     if (cols)
-        k_part_bin<L, SLOTS, true, TB, MK, MAXB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm,
-                                                                         ws.ntiles, slots);
+        k_part_bin<L, SLOTS, true, TB, MK, MAXB, kMinW><<<grid, TB, 0, stream>>>(
+            ks, mp, ws.pos, runs, sm, ws.ntiles, slots);
     else
-        k_part_bin<L, SLOTS, false, TB, MK, MAXB><<<grid, TB, 0, stream>>>(ks, mp, ws.pos, runs, sm,
-                                                                          ws.ntiles, slots);
+        k_part_bin<L, SLOTS, false, TB, MK, MAXB, kMinW><<<grid, TB, 0, stream>>>(
+            ks, mp, ws.pos, runs, sm, ws.ntiles, slots);
 }
 
 template <int L, bool SLOTS, int TB, int MK>
 void bin_launch_fast(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
-                     uint32_t *runs, const SegMap &sm, bool cols, unsigned grid, uint16_t *slots,
+                     uint32_t *runs, const SegMap &sm, bool cols, uint16_t *slots,
                      hipStream_t stream) {
     const size_t nb = ws.nbins;
     if constexpr (TB >= 1024) {
-        if (nb <= 1023) bin_launch<L, SLOTS, TB, MK, 1023>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
-        else if (nb <= 2047) bin_launch<L, SLOTS, TB, MK, 2047>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
-        else if (nb <= 4095) bin_launch<L, SLOTS, TB, MK, 4095>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
-        else bin_launch<L, SLOTS, TB, MK, (int)kPartMaxBinsBig>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        if (nb <= 1023) bin_launch<L, SLOTS, TB, MK, 1023>(ks, mp, ws, runs, sm, cols, slots, stream);
+        else if (nb <= 2047) bin_launch<L, SLOTS, TB, MK, 2047>(ks, mp, ws, runs, sm, cols, slots, stream);
+        else if (nb <= 4095) bin_launch<L, SLOTS, TB, MK, 4095>(ks, mp, ws, runs, sm, cols, slots, stream);
+        else bin_launch<L, SLOTS, TB, MK, (int)kPartMaxBinsBig>(ks, mp, ws, runs, sm, cols, slots, stream);
     } else {
-        if (nb <= 511) bin_launch<L, SLOTS, TB, MK, 511>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
-        else bin_launch<L, SLOTS, TB, MK, (int)kPartMaxBins>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+        if (nb <= 511) bin_launch<L, SLOTS, TB, MK, 511>(ks, mp, ws, runs, sm, cols, slots, stream);
+        else bin_launch<L, SLOTS, TB, MK, (int)kPartMaxBins>(ks, mp, ws, runs, sm, cols, slots, stream);
     }
 }
 
@@ -1419,7 +1419,6 @@ hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const Partition
                          uint16_t *slots, hipStream_t stream) {
     constexpr int kCap = TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
     if (ws.nbins > (size_t)kCap) return hipErrorInvalidValue;
-    const unsigned grid = part_bin_grid(ws.ntiles, TB);
     const bool cols = runs_as_columns(ws);
     uint32_t *runs = cols ? ws.run_starts : ws.run_rows;
     SegMap sm = seg_map_of(ws);
@@ -1437,25 +1436,25 @@ hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const Partition
         ks.layout == KEYS_ENTRY && (reinterpret_cast<uintptr_t>(ks.base) & 15) == 0;
     if (wide) {
         if (ks.layout == KEYS_PACKED)
-            bin_launch<KEYS_PACKED, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch<KEYS_PACKED, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
         else if (entry16)
-            bin_launch<KEYS_ENTRY, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch<KEYS_ENTRY, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
         else
-            bin_launch<KEYS_STRIDED, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch<KEYS_STRIDED, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
     } else if (p2) {
         if (ks.layout == KEYS_PACKED)
-            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModP2>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModP2>(ks, mp, ws, runs, sm, cols, slots, stream);
         else if (entry16)
-            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModP2>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModP2>(ks, mp, ws, runs, sm, cols, slots, stream);
         else
-            bin_launch<KEYS_STRIDED, SLOTS, TB, kModP2, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch<KEYS_STRIDED, SLOTS, TB, kModP2, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
     } else {
         if (ks.layout == KEYS_PACKED)
-            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModFast>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModFast>(ks, mp, ws, runs, sm, cols, slots, stream);
         else if (entry16)
-            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModFast>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModFast>(ks, mp, ws, runs, sm, cols, slots, stream);
         else
-            bin_launch<KEYS_STRIDED, SLOTS, TB, kModFast, kCap>(ks, mp, ws, runs, sm, cols, grid, slots, stream);
+            bin_launch<KEYS_STRIDED, SLOTS, TB, kModFast, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess || cols) return e;

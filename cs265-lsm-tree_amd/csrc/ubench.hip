@@ -155,6 +155,7 @@ extern "C" int ubench_run(int which, void *dbuf, size_t bytes, uint64_t m, int g
 // Geometry of the product's partition build of n keys into m bits
 // (tools/ubench.py sizes its buffers from it): segments, segment bits, tile
 // keys and tiles.
+// out4: segments, segment bits, tile keys, tiles.
 extern "C" int ubench_part_geometry(size_t n, uint64_t m, uint64_t *out4) {
     PartitionWorkspace ws{};
     if (!plan_segments(m, device_cu_count(), &ws)) return -34;
@@ -166,110 +167,40 @@ extern "C" int ubench_part_geometry(size_t n, uint64_t m, uint64_t *out4) {
     return 0;
 }
 
-// Phases of the product's partition build (tools/ubench.py part): variant 0 =
-// pass 1 (launch_part_bin: the product's tile, table layout and transpose),
-// 1 = pass 2 as the product launches it, G in {4, 8, 16, 32} = pass 2 with G
-// lanes per tile.  pos: ntiles * tile_keys u64; runs: both table layouts.
+// Phases of the product's partition build (tools/ubench.py part, p1ab):
+// 0 = pass 1 as the product launches it, 1 = pass 2 as the product launches
+// it over variant 0's output; 5001 / 5003 = pass-1 shapes (MINW waves per
+// SIMD, NWG workgroups per CU).  runs: both table layouts.
 extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, uint64_t *pos,
                            uint32_t *runs, uint32_t *words, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
     const ModParams mp = make_mod_params(m);
     PartitionWorkspace ws{};
-    // 40xx: segments planned for twice the CU count (two pass-2 workgroups per CU)
-    if (!plan_segments(m, (variant >= 4000 && variant < 4100 ? 2 : 1) * device_cu_count(), &ws))
-        return -34;
-    // forced tile sizes for the shape sweeps: 2048 keys (TB = 256 pass 1 and
-    // the 21xx pass-2 variants), 4096 keys (202x pass 1, 22xx pass 2)
-    const bool half = (variant >= 2004 && variant <= 2010) || (variant >= 2100 && variant < 2200);
-    const bool t4k = (variant >= 2020 && variant < 2100) || (variant >= 2200 && variant < 2300);
-    ws.tile_keys = half ? kPartTileKeys / 2 : t4k ? kPartTileKeys : choose_tile_keys(ws.nbins);
+    if (!plan_segments(m, device_cu_count(), &ws)) return -34;
+    ws.tile_keys = choose_tile_keys(ws.nbins);
     ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
     ws.pos = pos;
     ws.run_rows = runs;
     ws.run_starts = runs + ws.ntiles * (ws.nbins + 1);
-    const uint64_t nw32 = ((m + 63) / 64) * 2;
     hipError_t e = hipSuccess;
-    const bool big = ws.tile_keys == 2 * kPartTileKeys;
     switch (variant) {
-        case 0: case 4000: e = launch_part_bin(ks, mp, ws, s); break;
-        case 1: case 4001: e = launch_part_apply(mp, words, ws, 0, s); break;
-#define UB_G(G)                                                                                   \
-    case G:                                                                                       \
-        e = big ? launch_apply_g<kApplyBuild, G, 2 * (int)kPartTileKeys>(ws, m, words, nw32, 0,   \
-                                                                        nullptr, StackTable{}, s) \
-                : launch_apply_g<kApplyBuild, G, (int)kPartTileKeys>(ws, m, words, nw32, 0,       \
-                                                                    nullptr, StackTable{}, s);    \
-        break;
-        UB_G(4) UB_G(8) UB_G(16) UB_G(32)
-#undef UB_G
-#define UB_GD(G, D)                                                                               \
-    case 1000 + 10 * G + D:                                                                      \
-        e = big ? launch_apply_g<kApplyBuild, G, 2 * (int)kPartTileKeys, D>(ws, m, words, nw32, 0,  \
-                                                                           nullptr, StackTable{}, s) \
-                : launch_apply_g<kApplyBuild, G, (int)kPartTileKeys, D>(ws, m, words, nw32, 0,        \
-                                                                       nullptr, StackTable{}, s);    \
-        break;
-        UB_GD(1, 1) UB_GD(1, 2) UB_GD(1, 4) UB_GD(2, 1) UB_GD(2, 2) UB_GD(2, 4)
-        UB_GD(4, 1) UB_GD(4, 2) UB_GD(4, 4)
-#undef UB_GD
-#define UB_IG(G)                                                                                  \
-    case 3000 + G:                                                                               \
-        e = big ? launch_apply_g<kApplyBuild, G, 2 * (int)kPartTileKeys, 1, 1>(ws, m, words, nw32, \
-                                                                          0, nullptr, StackTable{}, s) \
-                : launch_apply_g<kApplyBuild, G, (int)kPartTileKeys, 1, 1>(ws, m, words, nw32, 0,  \
-                                                                      nullptr, StackTable{}, s); \
-        break;
-        UB_IG(1) UB_IG(2) UB_IG(4) UB_IG(8)
-#undef UB_IG
-        // pass-1 shapes: TB threads x 8 keys, histogram capacity MAXB, MINW
-        // waves per SIMD (register cap), NWG workgroups per CU
-#define UB_P1(V, TB, MAXB, MINW, NWG) UB_P1R(V, TB, MAXB, MINW, NWG, ws.run_rows)
-#define UB_P1R(V, TB, MAXB, MINW, NWG, RUNS)                                                     \
+        case 0: e = launch_part_bin(ks, mp, ws, s); break;
+        case 1: e = launch_part_apply(mp, words, ws, 0, s); break;
+        // pass-1 shapes with the p2 remainder (MINW, NWG)
+#define UB_P2(V, TB, MAXB, MINW, NWG)                                                             \
     case V: {                                                                                    \
-        if (ws.nbins > MAXB || ws.tile_keys != TB * kPartKPT) return -22;                        \
+        if (ws.nbins > MAXB || ws.tile_keys != TB * kPartKPT || !mp.p2) return -22;             \
         SegMap sm = seg_map_of(ws);                                                              \
-        sm.scaled_shift = sm.shift + mp.l;                                                       \
+        sm.p2_hi_shift = mp.p2t - sm.shift;                                                      \
         const unsigned g = (unsigned)std::min<size_t>(ws.ntiles, (size_t)device_cu_count() * NWG); \
-        k_part_bin<KEYS_PACKED, false, true, TB, kModFast, MAXB, MINW>                              \
-            <<<g, TB, 0, s>>>(ks, mp, ws.pos, RUNS, sm, ws.ntiles, nullptr);            \
+        k_part_bin<KEYS_PACKED, false, true, TB, kModP2, MAXB, MINW>                             \
+            <<<g, TB, 0, s>>>(ks, mp, ws.pos, ws.run_starts, sm, ws.ntiles, nullptr);            \
         e = hipGetLastError();                                                                   \
         break;                                                                                   \
     }
-        UB_P1(2001, 512, 1024, 4, 2) UB_P1(2002, 512, 1024, 5, 3) UB_P1(2003, 512, 1024, 6, 3)
-        UB_P1(2004, 256, 1024, 5, 5) UB_P1(2005, 256, 1024, 6, 5) UB_P1(2006, 256, 1024, 4, 4)
-        UB_P1(2007, 256, 511, 5, 5) UB_P1(2008, 256, 511, 6, 6)
-        UB_P1(2011, 512, 511, 4, 2) UB_P1(2012, 512, 511, 5, 3) UB_P1(2013, 512, 511, 6, 3)
-        UB_P1R(2014, 512, 511, 4, 2, ws.run_starts)
-        UB_P1(2021, 512, 1023, 4, 2) UB_P1(2022, 512, 4096, 4, 2)
-        UB_P1R(2015, 512, 511, 4, 2, ws.run_rows + 32)
-        UB_P1R(2016, 512, 511, 4, 2, ws.run_rows + 1024)
-#undef UB_P1
-#undef UB_P1R
-        // pass 2 over the 2048-key tiles the TB = 256 variants write (run_rows, columns)
-#define UB_H(G, D)                                                                                \
-    case 2100 + 10 * G + D: {                                                                    \
-        PartitionWorkspace w2 = ws;                                                              \
-        w2.run_starts = ws.run_rows;                                                             \
-        e = launch_apply_g<kApplyBuild, G, (int)kPartTileKeys / 2, D>(w2, m, words, nw32, 0,     \
-                                                                      nullptr, StackTable{}, s); \
-        break;                                                                                   \
-    }
-        UB_H(2, 2) UB_H(4, 1) UB_H(4, 2) UB_H(4, 4) UB_H(8, 2)
-#undef UB_H
-        // pass 2 over tables the 20xx / 202x pass-1 variants wrote (run_rows, columns)
-#define UB_HW(V, TK, G, D, W)                                                                     \
-    case V: {                                                                                    \
-        PartitionWorkspace w2 = ws;                                                              \
-        w2.run_starts = ws.run_rows;                                                             \
-        e = launch_apply_g<kApplyBuild, G, TK, D, W>(w2, m, words, nw32, 0, nullptr,              \
-                                                     StackTable{}, s);                           \
-        break;                                                                                   \
-    }
-        UB_HW(2191, 2048, 1, 1, 1) UB_HW(2192, 2048, 2, 1, 1) UB_HW(2194, 2048, 4, 1, 1)
-        UB_HW(2242, 4096, 4, 2, 0) UB_HW(2282, 4096, 8, 2, 0) UB_HW(2291, 4096, 1, 1, 1)
-        UB_HW(2292, 4096, 2, 1, 1) UB_HW(2294, 4096, 4, 1, 1)
-#undef UB_HW
+        UB_P2(5001, 512, 511, 4, 2) UB_P2(5003, 512, 511, 6, 3)
+#undef UB_P2
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

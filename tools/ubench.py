@@ -56,9 +56,8 @@ def _events(fn, reps):
     return a.elapsed_time(b) / reps
 
 
-def part_phases(n=16_777_216, bpe=10.0, reps=50):
-    """The product's partition build (C2 by default) by pass, and pass 2 with
-    each lane count G (ubench_part)."""
+def _part_setup(n, bpe):
+    """Keys, geometry and buffers of the product's partition build of n keys."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
     import bloomhip as bh
@@ -68,93 +67,68 @@ def part_phases(n=16_777_216, bpe=10.0, reps=50):
     assert LIB.ubench_part_geometry(n, m, geo.ctypes.data) == 0
     nbins, seg_bits, tk, ntiles = (int(x) for x in geo)
     pos = torch.empty(ntiles * tk, dtype=torch.int64, device="cuda")
-    runs = torch.empty(ntiles * (nbins + 1) * 4, dtype=torch.int32, device="cuda")  # room for the 2x-segment plans
+    runs = torch.empty(ntiles * (nbins + 1) * 2, dtype=torch.int32, device="cuda")
     words = torch.zeros((m + 63) // 64 * 2, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
 
     def run(v):
-        rc = LIB.ubench_part(v, keys.data_ptr(), n, m, pos.data_ptr(), runs.data_ptr(),
-                             words.data_ptr(), s.cuda_stream)
-        assert rc == 0, (v, rc)
-    names = {0: "pass 1", 1: "pass 2 (product G)", 4: "pass 2 G=4",
-             8: "pass 2 G=8", 16: "pass 2 G=16", 32: "pass 2 G=32",
-             3001: "pass 2 indep groups G=1", 3002: "pass 2 indep G=2", 3004: "pass 2 indep G=4",
-             3008: "pass 2 indep G=8"}
-    if os.environ.get("UB_P1"):
-        # order matters: the 21xx pass-2 variants read the table the last
-        # 2048-key-tile pass 1 (2007) wrote
-        names = {0: "pass 1", 2001: "pass 1 TB512 maxb1024 4w", 2002: "pass 1 TB512 maxb1024 5w 3wg",
-                 2003: "pass 1 TB512 maxb1024 6w 3wg", 2011: "pass 1 TB512 maxb511 4w",
-                 2013: "pass 1 TB512 maxb511 6w 3wg",
-                 2004: "pass 1 TB256 5w 5wg", 2006: "pass 1 TB256 4w 4wg",
-                 2008: "pass 1 TB256 maxb511 6w 6wg", 2007: "pass 1 TB256 maxb511 5w 5wg",
-                 2122: "pass 2 (2048-key tiles) G=2 d=2", 2142: "pass 2 (2048) G=4 d=2",
-                 2192: "pass 2 (2048) indep G=2", 2194: "pass 2 (2048) indep G=4",
-                 2191: "pass 2 (2048) indep G=1"}
-    if os.environ.get("UB_T4K"):  # C5 etc. on 4096-key tiles (TB = 512 pass 1)
-        names = {0: "pass 1 (product)", 1: "pass 2 (product)", 3002: "pass 2 indep G=2",
-                 3004: "pass 2 indep G=4",
-                 2021: "pass 1 TB512 4096-key tiles maxb1023", 2242: "pass 2 (4096) G=4 d=2",
-                 2282: "pass 2 (4096) G=8 d=2", 2291: "pass 2 (4096) indep G=1",
-                 2292: "pass 2 (4096) indep G=2", 2294: "pass 2 (4096) indep G=4",
-                 2022: "pass 1 TB512 4096-key tiles maxb4096"}
-    if os.environ.get("UB_GD"):
-        names = {0: "pass 1", 1: "pass 2 (product G)"}
-        names.update({1000 + 10 * g + d: f"pass 2 G={g} depth={d}"
-                      for g in (1, 2, 4) for d in (1, 2, 4)})
-    run(0)
-    # time-based prewarm: the chip's clocks ramp over the first ~0.1-0.5 s of
-    # work, which otherwise makes the first phases measured look slower
+        return LIB.ubench_part(v, keys.data_ptr(), n, m, pos.data_ptr(), runs.data_ptr(),
+                               words.data_ptr(), s.cuda_stream)
+    return run, words, {"n": n, "m": m, "nbins": nbins, "seg_bits": seg_bits, "tile_keys": tk}
+
+
+def _prewarm(run, v, secs=0.5):
     import time
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < float(os.environ.get("UB_PREWARM", "0.5")):
+    while time.perf_counter() - t0 < secs:
         for _ in range(20):
-            run(0)
+            run(v)
         torch.cuda.synchronize()
-    if os.environ.get("UB_P1"):
-        run(0); run(1)
-        ref = words.clone()
-        for p2 in (2142, 2192, 2194):
-            words.zero_(); run(2007); run(p2)
-            torch.cuda.synchronize()
-            print(json.dumps({"check": f"2048-key tiles {p2} bitmap == product", "ok": bool(torch.equal(ref, words))}))
-    if os.environ.get("UB_T4K"):
-        run(0); run(1)
-        ref = words.clone()
-        p1 = 2021 if nbins <= 1023 else 2022
-        for p2 in (2242, 2294):
-            words.zero_(); run(p1); run(p2)
-            torch.cuda.synchronize()
-            print(json.dumps({"check": f"4096-key tiles {p2} bitmap == product", "ok": bool(torch.equal(ref, words))}))
-    run(0); run(1)
+
+
+def part_phases(n=16_777_216, bpe=10.0, reps=50):
+    """The product's partition build by pass (pass 2 timed over pass 1's
+    output), two rounds."""
+    run, words, geo = _part_setup(n, bpe)
+    assert run(0) == 0 and run(1) == 0
+    torch.cuda.synchronize()
+    _prewarm(run, 0)
+    names = {0: "pass 1 (product)", 1: "pass 2 (product)"}
+    for rnd in range(2):
+        for v in (0, 1):
+            ms = _events(lambda: run(v), reps)
+            print(json.dumps({"op": "partition build", **geo, "phase": names[v], "round": rnd,
+                              "us": round(ms * 1e3, 1)}), flush=True)
+
+
+def p1_ab(variants, n=16_777_216, bpe=10.0, rounds=3, reps=50):
+    """Interleaved A/B of pass-1 variants (ubench_part 5xxx) against the
+    product (0): each variant's output goes through the product's pass 2
+    and must give the product's bitmap; then rounds x variants timed."""
+    run, words, geo = _part_setup(n, bpe)
+    assert run(0) == 0 and run(1) == 0
+    torch.cuda.synchronize()
     ref = words.clone()
-    for v in (3001, 3002, 3004, 3008):
-        words.zero_(); run(v)
+    ok_vars = [0]
+    for v in variants:
+        words.zero_()
+        if run(v) != 0:
+            print(json.dumps({"variant": v, "skipped": "not applicable"}), flush=True)
+            continue
+        run(1)
         torch.cuda.synchronize()
-        print(json.dumps({"check": f"indep walk {v} bitmap == product", "ok": bool(torch.equal(ref, words))}), flush=True)
-    if os.environ.get("UB_QUICK"):
-        names = {0: "pass 1", 1: "pass 2 (product)"}
-    if os.environ.get("UB_2X"):  # segments for twice the CU count (two pass-2 WGs per CU)
-        run(4000); run(4001)
-        w2 = words.clone()
-        run(0); run(1)
-        print(json.dumps({"check": "2x-segment plan bitmap == product", "ok": bool(torch.equal(w2, words))}), flush=True)
-        names = {0: "pass 1", 1: "pass 2 (product)", 4000: "pass 1 (2x segments)",
-                 4001: "pass 2 (2x segments)", -4000: "pass 1 (2x) again", -5: "pass 2 again",
-                 -4001: "pass 2 (2x) again"}
-    names = dict(names)
-    names[-1] = "pass 1 (again, last)"
-    if os.environ.get("UB_ALT"):
-        names = {0: "pass 1 product", 2014: "2011 at run_starts", -1: "product", -2014: "2011 again",
-                 -2: "product", -3: "2011 again"}
-    for v, name in names.items():
-        ms = _events(lambda: run({-1: 0, -2: 0, -3: 2014, -5: 1}.get(v, abs(v))), reps)
-        print(json.dumps({"op": "partition build", "n": n, "m": m, "nbins": nbins,
-                          "seg_bits": seg_bits, "tile_keys": tk, "phase": name,
-                          "us": round(ms * 1e3, 1)}), flush=True)
-
-
-
+        ok = bool(torch.equal(ref, words))
+        print(json.dumps({"check": f"pass-1 variant {v} bitmap == product", "ok": ok}), flush=True)
+        if ok:
+            ok_vars.append(v)
+    _prewarm(run, 0)
+    res = {v: [] for v in ok_vars}
+    for _ in range(rounds):
+        for v in res:
+            res[v].append(round(_events(lambda: run(v), reps) * 1e3, 2))
+    for v, ts in res.items():
+        print(json.dumps({"op": "pass 1 A/B", **geo, "variant": v, "us": ts, "min_us": min(ts)}),
+              flush=True)
 
 
 def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
@@ -246,6 +220,9 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "stack":
         stack_ablation()
         return stack_ablation((0, 1, 2, 3))
+    if len(sys.argv) > 1 and sys.argv[1] == "p1ab":
+        vs = [int(v) for v in os.environ.get("UB_VARIANTS", "5001,5003").split(",")]
+        return p1_ab(vs)
     if len(sys.argv) > 1 and sys.argv[1] == "part":
         return part_phases()
     if len(sys.argv) > 1 and sys.argv[1] == "part_c5":
