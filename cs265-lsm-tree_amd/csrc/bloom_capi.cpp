@@ -713,7 +713,7 @@ namespace {
 // per 2^24 keys on MI355X (C3's level filters, tools/probe_sweep.py): what
 // AUTO weighs before stacking a group.
 constexpr double kCostLds = 70, kCostGatherL2 = 125, kCostGatherFar = 530, kCostPartition = 250,
-                 kCostStacked = 230;
+                 kCostStacked = 230, kCostLadder = 170;
 
 double probe_cost_alone(const bloomhip_filter *f, size_t n) {
     switch (probe_kind(f, BLOOMHIP_PROBE_AUTO, n)) {
@@ -762,12 +762,18 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
             g = std::gcd(g, filters[j]->m);
             alone += probe_cost_alone(filters[j], n);
         }
+        // A ladder (members d << t_j: an LSM's levels at a power-of-two
+        // fanout) bins by hash bits, else segments of m_max.
         PartitionWorkspace ws{};
-        if (!plan_stack(mh, g, mmin, (int)mem.size(), ncu, &ws)) continue;
-        if (!explicit_stack && (mem.size() < 2 || n < kProbePartitionMinKeys ||
-                                ws.nbins < (size_t)ncu || alone <= kCostStacked))
-            continue;
         StackTable st{};
+        uint64_t msz[kMaxStack];
+        for (size_t k = 0; k < mem.size(); k++) msz[k] = filters[mem[k]]->m;
+        const bool ladder = plan_ladder(msz, (int)mem.size(), ncu, &st, &ws);
+        if (!ladder && !plan_stack(mh, g, mmin, (int)mem.size(), ncu, &ws)) continue;
+        if (!explicit_stack && (mem.size() < 2 || n < kProbePartitionMinKeys ||
+                                ws.nbins < (size_t)ncu ||
+                                alone <= (ladder ? kCostLadder : kCostStacked)))
+            continue;
         st.nf = (int)mem.size();
         for (int k = 0; k < st.nf; k++) {
             st.words[k] = filters[mem[k]]->d_words;

@@ -83,11 +83,13 @@ static_assert(kStackMaxBits <= (1u << kEntryBits), "segment offsets fit an entry
 // b = mulhi(x, magic) = (x >> 1) / group.  magic = ceil(2^31 / group) (2^31
 // for group 1), checked exact for every x < 2 * nsub when planned.
 struct SegMap {
-    uint32_t shift;  // sub_shift - 1
+    uint32_t shift;  // sub_shift - 1 (ladder: s, the bin's lowest hash bit)
     uint32_t magic;
     uint32_t nbins;
     uint32_t scaled_shift;  // shift + l: the same map on a remainder scaled by 2^l (mod_fast_scaled)
     uint32_t p2_hi_shift;   // t - shift: where (x >> t) % d lands in p >> shift (m = d << t)
+    uint32_t lad_u;         // ladder: log2(nbins), the bin's hash bits [s, s + u)
+    uint32_t lad_hb;        // ladder: t_max - s - u, hash bits [s + u, t_max) kept in the entry
 };
 
 struct PartitionWorkspace {
@@ -102,10 +104,14 @@ struct PartitionWorkspace {
     uint32_t seg_bits;     // S = group << sub_shift
     uint32_t tile_keys;    // keys per pass-1 tile: kPartTileKeys, or twice that (0 = default)
     uint32_t magic;        // SegMap::magic
+    uint32_t lad_s;        // ladder stack (StackTable::lad): bins are hash bits [s, s + u);
+    uint32_t lad_u;        //   0 for every other partition pass
+    uint32_t lad_hb;
 };
 
 inline SegMap seg_map_of(const PartitionWorkspace &ws) {
-    return SegMap{ws.sub_shift - 1, ws.magic, (uint32_t)ws.nbins, 0, 0};
+    if (ws.lad_u) return SegMap{ws.lad_s, 0, (uint32_t)ws.nbins, 0, 0, ws.lad_u, ws.lad_hb};
+    return SegMap{ws.sub_shift - 1, ws.magic, (uint32_t)ws.nbins, 0, 0, 0, 0};
 }
 
 // Keys per pass-1 tile for a batch sorted into nbins segments: short runs
@@ -157,12 +163,64 @@ constexpr size_t kProbePartitionMinKeys = 1u << 18;
 // (bit j = member j's bit); the combine ANDs each key's three bytes.
 constexpr int kMaxStack = 8;
 
+// Ladder stack: every member is m_j = d << t_j with the same odd d | 255
+// (the p2 form of bloom_math.h) -- an LSM's levels at a power-of-two fanout
+// (C3: d = 5, t_j = 17, 19, ..., 25).  Then x % m_j = a_j << t_j | (x mod
+// 2^t_j) with a_j = (x >> t_j) % d, and a_j follows from the largest
+// member's a_max and the hash bits between: a_j = (a_max * 2^(t_max - t_j) +
+// bits [t_j, t_max) of x) % d.  Pass 1 bins positions by hash bits [s, s+u)
+// (2^u = 256 bins, one per CU, s <= t_min, s + u <= t_max) and keeps the
+// entry e = (a_max << hb | bits [s+u, t_max)) << s | bits [0, s), hb =
+// t_max - s - u.  For bin b every member's bits that such an entry can
+// reach are whole blocks of 2^s bits: member j's block i is
+//   t_j >= s+u: a = i >> (t_j-s-u), h = i mod 2^(t_j-s-u): bits from
+//               a << t_j | h << (s+u) | b << s,
+//   t_j <  s+u: a = i: bits from a << t_j | (b mod 2^(t_j - s)) << s,
+// (d << max(0, t_j - s - u) blocks).  Members 0 .. k-1 ("direct") have
+// their blocks staged in LDS (block q at LDS word q * 2^(s-5)); the smaller
+// members k .. nf-1 ("packed") are merged into one image of bpp (4 or 8)
+// bits per position: for each block i of member k (a "tuple": every smaller
+// member's block follows from it and the bin), position p holds bit j - k =
+// member j's bit, so one LDS read answers all packed members.  A table
+// from e >> s (member 0's block) gives the LDS byte addresses of the other
+// direct members' blocks and of the packed image's tuple (one word each, rs
+// words per row).  Runs are as long as the build's (256 bins
+// instead of the segment stack's 1,280 at C3) and each member bit is staged
+// once per bin.
+struct LadderTable {
+    uint32_t s, u, hb, d;       // geometry as above
+    uint32_t ne;                // d << hb: entry high parts (table rows)
+    uint32_t k;                 // direct members (1 .. nf)
+    uint32_t bpp;               // packed bits per position: 4 or 8 (0: none, k == nf)
+    uint32_t pk_words;          // LDS word where the packed image starts (tuple-aligned)
+    uint32_t img_words;         // LDS words of the direct blocks + packed image (the table follows)
+    uint32_t rs;                // table row stride in words: 1, 2, 4 or 8
+    uint32_t t[kMaxStack];      // member j is d << t[j] (member 0 the largest)
+    uint32_t nblk[kMaxStack];   // member j's blocks per bin (packed members: tuples = nblk[k])
+    uint32_t base[kMaxStack];   // direct member j's first block in the image
+    uint32_t pmod[kMaxStack];   // 2^(t_max - t_j) % d
+    uint32_t pmodk[kMaxStack];  // 2^(t_k - t_j) % d (packed members j > k)
+};
+
 struct StackTable {
     const uint32_t *words[kMaxStack];  // member bitmaps (32-bit word view)
     uint32_t mwords[kMaxStack];        // m_j / 32: member j's size in words (m_j % 128 == 0)
     int row[kMaxStack];                // output row of member j
     int nf;
+    int ladder;                        // 1: lad holds a ladder geometry (plan_ladder)
+    LadderTable lad;
 };
+
+// Ladder geometry for members m[0] >= m[1] >= ... (all d << t_j with one d):
+// fills st->lad / st->ladder and the workspace's bins; false when the members
+// do not form a ladder or no (s, u) fits the LDS image, the entry's 21 bits
+// and the table.  ncu sets u (2^u >= ncu bins).
+bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWorkspace *ws);
+// LDS bytes of a ladder pass 2: the images, the table, and the tuple map
+// (tuple -> packed members' blocks) used while the packed image is built.
+inline size_t ladder_lds_bytes(const LadderTable &l) {
+    return (size_t)l.img_words * 4 + (size_t)l.ne * l.rs * 4 + (l.bpp ? (size_t)l.nblk[l.k] * 32 : 0);
+}
 
 
 // Kernels enqueued on `stream`; all return hipSuccess or the launch error.

@@ -180,6 +180,24 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// LDS word at an absolute byte address.  Pass 2 has no static LDS, so its
+// dynamic image starts at LDS address 0 (launch_apply_g checks that once per
+// kernel) and image offsets are addresses: a pointer formed from the image's
+// generic pointer costs a v_add of its relocated address (0) per access.
+__device__ __forceinline__ uint32_t lds_word(uint32_t byte_addr) {
+    return *(const __attribute__((address_space(3))) uint32_t *)(size_t)byte_addr;
+}
+typedef uint32_t lds_v2u __attribute__((ext_vector_type(2)));
+typedef uint32_t lds_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint2 lds_word2(uint32_t byte_addr) {
+    const lds_v2u v = *(const __attribute__((address_space(3))) lds_v2u *)(size_t)byte_addr;
+    return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint4 lds_word4(uint32_t byte_addr) {
+    const lds_v4u v = *(const __attribute__((address_space(3))) lds_v4u *)(size_t)byte_addr;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 template <bool B>
 struct BoolC {
     static constexpr bool value = B;
@@ -263,7 +281,7 @@ constexpr uint32_t kBinShift = 19;  // 8192 segments << 19 < 2^32
 // (b = 0..nbins): COLS = true: straight into the segment-major table
 // runs[b * ntiles + tile]; COLS = false: into the tile-major
 // runs[tile * (nbins + 1) + b], for k_runs_transpose (large tables).
-constexpr int kModFast = 0, kModWide = 1, kModP2 = 2;
+constexpr int kModFast = 0, kModWide = 1, kModP2 = 2, kModLadder = 3;
 
 template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4>
 __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
@@ -319,6 +337,16 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                         const uint64_t p = mod_wide(raw, mp);
                         b = seg_of(p, sm);
                         ent[3 * j + h] = (uint32_t)p & kEntryMask;
+                    } else if constexpr (MK == kModLadder) {
+                        // ladder stack (StackTable::lad): bin = hash bits
+                        // [s, s+u), entry = (a_max << hb | bits [s+u, t_max))
+                        // << s | bits [0, s) with a_max = (x >> t_max) % d
+                        const uint32_t xl = (uint32_t)raw;
+                        const uint32_t a = mod_p2_hi(raw, mp);
+                        b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
+                        const uint32_t ehi =
+                            (a << sm.lad_hb) + __builtin_amdgcn_ubfe(xl, sm.scaled_shift, sm.lad_hb);
+                        ent[3 * j + h] = (ehi << sm.shift) | __builtin_amdgcn_ubfe(xl, 0, sm.shift);
                     } else if constexpr (MK == kModP2) {
                         const uint32_t xl = (uint32_t)raw;
                         const uint32_t r = mod_p2_hi(raw, mp);
@@ -534,10 +562,10 @@ inline int apply_lanes_per_tile(size_t nbins, size_t tile_pos = kPartTilePos) {
 // twice.  A wave owns batches of kApplyDepth load groups; the next batch's
 // run bounds are loaded while the current one is applied, and the rare tile
 // whose run outlasts the first step is finished by a wave-uniform loop.
-constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2;
+constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2, kApplyLadder = 3;
 
 template <int MODE, int G, int TILE_KEYS, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth,
-          int WALK = 0, int NF = 0>
+          int WALK = 0, int NF = 0, int LK = 0>
 __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const uint64_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, uint32_t seg_bits, uint64_t m, uint32_t *__restrict__ words, uint64_t nw32,
@@ -581,6 +609,122 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                 dst[nf] = v.y;
                 dst[2 * nf] = v.z;
                 dst[3 * nf] = v.w;
+            }
+        }
+    } else if constexpr (MODE == kApplyLadder) {
+        // bin b's blocks of the direct members (StackTable::lad), block q at
+        // LDS word q << (s - 5); the table: row e (member 0's block, the
+        // entry's bits above s) holds, one byte each, the other direct
+        // members' blocks and the packed image's tuple; the tuple map: per
+        // tuple, the first bit of each packed member's block; then the packed
+        // image, bpp bits per position and tuple.
+        const LadderTable &L = st.lad;
+        constexpr uint32_t K = LK;  // direct members (L.k, compiled in)
+        constexpr uint32_t BPP = (uint32_t)NF - K <= 4 ? 4u : 8u;
+        const uint32_t bv = L.s - 7;  // log2 of 16-B vectors per block
+        const uint32_t bin = (uint32_t)b;
+        // first bit of block i of member j for this bin
+        auto first_bit = [&](uint32_t j, uint32_t i) -> uint32_t {
+            const uint32_t tj = L.t[j];
+            if (tj >= L.s + L.u) {
+                const uint32_t hj = tj - L.s - L.u;
+                return ((i >> hj) << tj) + ((i & ((1u << hj) - 1u)) << (L.s + L.u)) + (bin << L.s);
+            }
+            return (i << tj) + ((bin & ((1u << (tj - L.s)) - 1u)) << L.s);
+        };
+        // block of member j given a = (x >> t_j) % d and xs = hash bits [s, t)
+        // for some t >= t_j (bits [s + u, t_j) of x are bits [u, t_j - s) of xs)
+        auto block_of = [&](uint32_t j, uint32_t aj, uint32_t xs) -> uint32_t {
+            const uint32_t tj = L.t[j];
+            if (tj < L.s + L.u) return aj;
+            const uint32_t hj = tj - L.s - L.u;
+            return (aj << hj) | ((xs >> L.u) & ((1u << hj) - 1u));
+        };
+        for (uint32_t j = 0; j < K; j++) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(st.words[j]);
+            uint4 *dst = reinterpret_cast<uint4 *>(seg) + ((size_t)L.base[j] << bv);
+            for (uint32_t q = threadIdx.x; q < (L.nblk[j] << bv); q += BLOCK)
+                dst[q] = src[(first_bit(j, q >> bv) >> 7) + (q & ((1u << bv) - 1u))];
+        }
+        uint32_t *tbl = seg + L.img_words;
+        uint32_t *tmap = tbl + L.ne * L.rs;
+        constexpr uint32_t kTupleShift = BPP == 4 ? 0u : 1u;  // tuple words = 2^(s-3+this)
+        for (uint32_t e = threadIdx.x; e < L.ne; e += BLOCK) {
+            const uint32_t amax = e >> L.hb;
+            const uint32_t xs = ((e & ((1u << L.hb) - 1u)) << L.u) | bin;  // hash bits [s, t_max)
+            for (uint32_t j = 1; j < (uint32_t)NF && j <= K; j++) {
+                const uint32_t tj = L.t[j];
+                const uint32_t aj = (amax * L.pmod[j] + (xs >> (tj - L.s)) % L.d) % L.d;
+                const uint32_t ij = block_of(j, aj, xs);
+                // direct member j: its block's LDS byte address; member K:
+                // the packed tuple's
+                tbl[e * L.rs + (j - 1)] = j < K ? (L.base[j] + ij) << (L.s - 3)
+                                                : (L.pk_words + (ij << (L.s - 3 + kTupleShift))) << 2;
+            }
+        }
+        if constexpr (K < (uint32_t)NF) {
+            const uint32_t tk = L.t[K], ntup = L.nblk[K];
+            for (uint32_t tp = threadIdx.x; tp < ntup; tp += BLOCK) {
+                // tuple tp = member K's block: a_K and hash bits [s, t_K)
+                uint32_t ak, xs;
+                if (tk >= L.s + L.u) {
+                    const uint32_t hk = tk - L.s - L.u;
+                    ak = tp >> hk;
+                    xs = ((tp & ((1u << hk) - 1u)) << L.u) | bin;
+                } else {
+                    ak = tp;
+                    xs = bin & ((1u << (tk - L.s)) - 1u);
+                }
+                for (uint32_t j = K; j < (uint32_t)NF; j++) {
+                    const uint32_t aj = (ak * L.pmodk[j] + (xs >> (L.t[j] - L.s)) % L.d) % L.d;
+                    tmap[8 * tp + (j - K)] = first_bit(j, block_of(j, aj, xs));
+                }
+            }
+        }
+        __syncthreads();
+        if constexpr (K < (uint32_t)NF) {
+            // packed image: thread task = (tuple, 32 positions): one 32-bit
+            // read per packed member, spread to bpp-bit fields
+            const uint32_t cps = 1u << (L.s - 5);  // 32-position chunks per tuple
+            const uint32_t ntask = L.nblk[K] * cps;
+            uint32_t *pk = seg + L.pk_words;
+            for (uint32_t q = threadIdx.x; q < ntask; q += BLOCK) {
+                const uint32_t tp = q >> (L.s - 5), c = q & (cps - 1u);
+                uint32_t w[NF];
+#pragma unroll
+                for (int j = 0; j < NF; j++)
+                    w[j] = (uint32_t)j >= K ? st.words[j][(tmap[8 * tp + (j - K)] >> 5) + c] : 0u;
+                uint32_t *dst = pk + q * BPP;
+                if constexpr (BPP == 4) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        uint32_t o = 0;
+#pragma unroll
+                        for (int j = 0; j < NF; j++) {
+                            if ((uint32_t)j < K) continue;
+                            uint32_t x = (w[j] >> (8 * r)) & 0xFFu;  // positions 8r .. 8r+7
+                            x = (x | (x << 12)) & 0x000F000Fu;
+                            x = (x | (x << 6)) & 0x03030303u;
+                            x = (x | (x << 3)) & 0x11111111u;  // bit i at 4i
+                            o |= x << (j - K);
+                        }
+                        dst[r] = o;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 8; r++) {
+                        uint32_t o = 0;
+#pragma unroll
+                        for (int j = 0; j < NF; j++) {
+                            if ((uint32_t)j < K) continue;
+                            uint32_t x = (w[j] >> (4 * r)) & 0xFu;  // positions 4r .. 4r+3
+                            x = (x | (x << 14)) & 0x00030003u;
+                            x = (x | (x << 7)) & 0x01010101u;  // bit i at 8i
+                            o |= x << (j - K);
+                        }
+                        dst[r] = o;
+                    }
+                }
             }
         }
     } else if constexpr (MODE == kApplyProbe) {
@@ -627,7 +771,10 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             // Branch-free: the run's entries among the six form the 6-bit
             // mask vm; an entry outside the run ORs 0.  The word's LDS byte
             // address is ((e - base) mod 2^21) / 32 * 4 (the segment image
-            // starts at LDS address 0: the kernel has no static LDS) and the
+            // starts at LDS address 0: the kernel has no static LDS, which
+            // launch_apply_g checks before the first launch; an address
+            // taken from seg's pointer costs a v_add of the image's
+            // relocated address, 0, per entry) and the
             // bit index the low 5 bits of e - base, which the shift takes as
             // they are.
             const int s0 = (int)(6 * vi) - (int)r.x;          // entry 0's place in the run
@@ -648,6 +795,62 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             for (int k = 0; k < 6; k++) {
                 const uint32_t ok = i0 + k < len ? 1u : 0u;
                 mask |= ok << k;
+                if constexpr (MODE == kApplyLadder) {
+                    // member 0's block is the entry's high part (its blocks
+                    // come first at LDS 0, 2^(s-3) bytes each), so its word's
+                    // byte address is (e >> 3) & ~3; the table row gives the
+                    // other direct members' block addresses and the packed
+                    // tuple's (block and tuple bases are aligned, so the
+                    // offsets OR in).  Bit extracts take the entry itself
+                    // as the shift: v_bfe_u32 uses its low 5 bits.
+                    const LadderTable &L = st.lad;
+                    constexpr int K = LK;  // direct members, compiled in
+                    const uint32_t ee = ok ? e[k] : 0u;  // reads stay in the image
+                    const uint32_t a0 = (ee >> 3) & ~3u;
+                    uint32_t acc = __builtin_amdgcn_ubfe(lds_word(a0), ee, 1u);
+                    if constexpr (K > 1 || K < NF) {
+                        constexpr int RW = (K - 1) + (K < NF ? 1 : 0);  // row words used
+                        constexpr int RS = RW <= 1 ? 1 : RW <= 2 ? 2 : RW <= 4 ? 4 : 8;  // = L.rs
+                        const uint32_t row = L.img_words * 4 + (ee >> L.s) * (4 * RS);  // byte address
+                        uint32_t rw[RW];
+                        if constexpr (RW == 1) {
+                            rw[0] = lds_word(row);
+                        } else if constexpr (RW == 2) {
+                            const uint2 v2 = lds_word2(row);
+                            rw[0] = v2.x;
+                            rw[1] = v2.y;
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < RW; q += 4) {
+                                const uint4 v4 = lds_word4(row + 4 * q);
+                                const uint32_t vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+                                for (int r = 0; r < 4; r++)
+                                    if (q + r < RW) rw[q + r] = vv[r];
+                            }
+                        }
+                        const uint32_t wmask = (1u << (L.s - 3)) - 4u;  // word offset in a block
+#pragma unroll
+                        for (int j = 1; j < K; j++) {
+                            const uint32_t wj = lds_word((a0 & wmask) | rw[j - 1]);
+                            acc |= __builtin_amdgcn_ubfe(wj, ee, 1u) << j;
+                        }
+                        if constexpr (K < NF) {
+                            uint32_t pa, psh;
+                            if constexpr (NF - K <= 4) {  // 8 positions per word: (lo >> 3) words
+                                pa = ((ee >> 1) & ((1u << (L.s - 1)) - 4u)) | rw[K - 1];
+                                psh = ee << 2;
+                            } else {  // 4 positions per word: (lo >> 2) words
+                                pa = (ee & ((1u << L.s) - 4u)) | rw[K - 1];
+                                psh = ee << 3;
+                            }
+                            const uint32_t pw = lds_word(pa);
+                            acc |= __builtin_amdgcn_ubfe(pw, psh, (uint32_t)(NF - K)) << K;
+                        }
+                    }
+                    bits[k] = acc;
+                    continue;
+                }
                 const uint32_t o = ok ? (e[k] - base21) & kEntryMask : 0u;  // reads stay in the image
                 if constexpr (MODE == kApplyStack) {
                     const uint32_t sh = o & 31;
@@ -1347,6 +1550,93 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
     return true;
 }
 
+// Ladder geometry (kernels.h LadderTable).  Of the (s, k) that fit -- the
+// entry (s bits + member 0's block index) in 21 bits, byte-sized table
+// fields (block indexes of direct members 1.. and tuples < 256), images +
+// table + tuple map in 160 KiB -- the fewest LDS reads per entry (k direct
+// members, one packed word, one table row), then the smallest image, then
+// the widest blocks.  Pass 1 tiles of 8192 keys: runs of ~96 entries per bin.
+constexpr uint32_t kLadderTileKeys = 2 * (uint32_t)kPartTileKeys;
+
+bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWorkspace *ws) {
+    if (nf < 2 || nf > kMaxStack) return false;
+    uint32_t d = 0, t[kMaxStack];
+    for (int j = 0; j < nf; j++) {
+        uint32_t dj = 0, tj = 0;
+        if (!p2_form(m[j], &dj, &tj) || (j > 0 && (dj != d || tj > t[j - 1]))) return false;
+        d = dj;
+        t[j] = tj;
+    }
+    const uint32_t tmax = t[0], tmin = t[nf - 1];
+    uint32_t u = 1;
+    while ((1u << u) < (uint32_t)(ncu > 2 ? ncu : 2)) u++;
+    if (u > 12 || tmax < u + 7) return false;
+    auto pow2mod = [&](uint32_t e) {
+        uint32_t pm = 1 % d;
+        for (uint32_t q = 0; q < e; q++) pm = (pm * 2) % d;
+        return pm;
+    };
+    LadderTable best{};
+    size_t best_bytes = 0;
+    uint32_t best_reads = ~0u;
+    for (uint32_t s = 7; s <= tmin && s + u <= tmax; s++) {
+        for (uint32_t k = 1; k <= (uint32_t)nf; k++) {
+            if (k > 3 && k < (uint32_t)nf) continue;  // the compiled-in direct counts
+            LadderTable L{};
+            L.s = s;
+            L.u = u;
+            L.hb = tmax - s - u;
+            L.d = d;
+            L.k = k;
+            if (L.hb > 16) continue;
+            L.ne = d << L.hb;
+            uint32_t ebits = 0;
+            while ((1u << ebits) < L.ne) ebits++;
+            if (s + ebits > kEntryBits) continue;
+            bool ok = true;
+            uint32_t nb = 0;
+            for (int j = 0; j < nf; j++) {
+                L.t[j] = t[j];
+                L.nblk[j] = t[j] >= s + u ? d << (t[j] - s - u) : d;
+                L.pmod[j] = pow2mod(tmax - t[j]);
+                L.pmodk[j] = (uint32_t)j >= k ? pow2mod(t[k] - t[j]) : 0u;
+                if ((uint32_t)j < k) {
+                    L.base[j] = nb;
+                    nb += L.nblk[j];
+                }
+            }
+            L.img_words = nb << (s - 5);
+            if (k < (uint32_t)nf) {
+                L.bpp = nf - (int)k <= 4 ? 4 : 8;
+                const uint32_t tuple_words = L.bpp << (s - 5);
+                L.pk_words = (L.img_words + tuple_words - 1) / tuple_words * tuple_words;
+                L.img_words = L.pk_words + L.nblk[k] * tuple_words;
+            }
+            const uint32_t rw = (k - 1) + (k < (uint32_t)nf ? 1 : 0);
+            L.rs = rw <= 1 ? 1 : rw <= 2 ? 2 : rw <= 4 ? 4 : 8;
+            if (!ok) continue;
+            const size_t bytes = ladder_lds_bytes(L);
+            if (bytes > kStackMaxBits / 8) continue;
+            const uint32_t reads = k + (k < (uint32_t)nf) + (k > 1 || k < (uint32_t)nf);
+            if (reads < best_reads || (reads == best_reads && bytes <= best_bytes)) {
+                best = L;  // ascending s: ties keep the wider blocks
+                best_bytes = bytes;
+                best_reads = reads;
+            }
+        }
+    }
+    if (best_bytes == 0) return false;
+    st->ladder = 1;
+    st->lad = best;
+    ws->nbins = (size_t)1 << u;
+    ws->lad_s = best.s;
+    ws->lad_u = best.u;
+    ws->lad_hb = best.hb;
+    ws->seg_bits = 0;
+    ws->tile_keys = kLadderTileKeys;
+    return true;
+}
+
 hipError_t launch_runs_transpose(const PartitionWorkspace &ws, hipStream_t stream) {
     const int width = (int)ws.nbins + 1;
     const dim3 grid((unsigned)((width + kTransposeTile - 1) / kTransposeTile),
@@ -1430,10 +1720,24 @@ hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const Partition
             sm.magic = 0;
         }
     }
-    const bool p2 = p2_pass1(mp, sm);
-    if (p2) sm.p2_hi_shift = mp.p2t - sm.shift;
     const bool entry16 =
         ks.layout == KEYS_ENTRY && (reinterpret_cast<uintptr_t>(ks.base) & 15) == 0;
+    if (ws.lad_u) {  // ladder stack: bins are hash bits [s, s + u) (plan_ladder)
+        if (!mp.fast || !mp.p2 || sm.shift + sm.lad_u + sm.lad_hb != mp.p2t)
+            return hipErrorInvalidValue;
+        sm.scaled_shift = sm.shift + sm.lad_u;
+        if (ks.layout == KEYS_PACKED)
+            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModLadder>(ks, mp, ws, runs, sm, cols, slots, stream);
+        else if (entry16)
+            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModLadder>(ks, mp, ws, runs, sm, cols, slots, stream);
+        else
+            bin_launch<KEYS_STRIDED, SLOTS, TB, kModLadder, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess || cols) return e;
+        return launch_runs_transpose(ws, stream);
+    }
+    const bool p2 = p2_pass1(mp, sm);
+    if (p2) sm.p2_hi_shift = mp.p2t - sm.shift;
     if (wide) {
         if (ks.layout == KEYS_PACKED)
             bin_launch<KEYS_PACKED, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
@@ -1479,22 +1783,28 @@ hipError_t launch_part_bin(const KeySpan &ks, const ModParams &mp, const Partiti
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
-template <int MODE, int G, int TK, int DEPTH = kApplyDepth, int WALK = 0, int NF = 0>
+template <int MODE, int G, int TK, int DEPTH = kApplyDepth, int WALK = 0, int NF = 0, int LK = 0>
 hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                           uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                           hipStream_t stream) {
     if (NF && st.nf != NF) return hipErrorInvalidValue;
-    static const bool attr_set = [] {
-        (void)hipFuncSetAttribute(
-            reinterpret_cast<const void *>(&k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK, NF>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+    // The build's walk addresses the segment image by absolute LDS byte
+    // address, which is right only while the dynamic image starts at LDS
+    // address 0, i.e. while the kernel has no static LDS: checked once per
+    // instantiation from the code object, and the launch refused otherwise.
+    static const bool lds_ok = [] {
+        const void *fn =
+            reinterpret_cast<const void *>(&k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK, NF, LK>);
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kStackMaxBits / 8));
-        return true;
+        hipFuncAttributes fa{};
+        return hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.sharedSizeBytes == 0;
     }();
-    (void)attr_set;
-    const size_t lds = (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
+    if (!lds_ok) return hipErrorInvalidDeviceFunction;
+    const size_t lds = MODE == kApplyLadder ? ladder_lds_bytes(st.lad)
+                                            : (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
     if (lds > kStackMaxBits / 8) return hipErrorInvalidValue;
-    k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK, NF><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
+    k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK, NF, LK><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
         res, st);
     return hipGetLastError();
@@ -1514,25 +1824,64 @@ hipError_t launch_stack_nf(const PartitionWorkspace &ws, uint64_t m, uint8_t *re
     }
 }
 
+// The ladder's pass 2 with the member count and the direct members (plan_ladder:
+// 1, 2, 3 or all of them) compiled in.
+template <int G, int TK, int WALK, int N, int D = kApplyDepth>
+hipError_t launch_ladder_k(const PartitionWorkspace &ws, uint64_t m, uint8_t *res,
+                           const StackTable &st, hipStream_t stream) {
+    switch (st.lad.k) {
+        case 1: return launch_apply_g<kApplyLadder, G, TK, D, WALK, N, 1>(ws, m, nullptr, 0, 0, res, st, stream);
+        case 2: return launch_apply_g<kApplyLadder, G, TK, D, WALK, N, 2>(ws, m, nullptr, 0, 0, res, st, stream);
+        case 3:
+            if constexpr (N >= 3)
+                return launch_apply_g<kApplyLadder, G, TK, D, WALK, N, 3>(ws, m, nullptr, 0, 0, res, st, stream);
+            else
+                return hipErrorInvalidValue;
+        default:
+            if (st.lad.k != (uint32_t)N) return hipErrorInvalidValue;
+            return launch_apply_g<kApplyLadder, G, TK, D, WALK, N, N>(ws, m, nullptr, 0, 0, res, st, stream);
+    }
+}
+
+template <int G, int TK, int WALK = 1, int D = kApplyDepth>
+hipError_t launch_ladder_nf(const PartitionWorkspace &ws, uint64_t m, uint8_t *res,
+                            const StackTable &st, hipStream_t stream) {
+    switch (st.nf) {
+        case 2: return launch_ladder_k<G, TK, WALK, 2, D>(ws, m, res, st, stream);
+        case 3: return launch_ladder_k<G, TK, WALK, 3, D>(ws, m, res, st, stream);
+        case 4: return launch_ladder_k<G, TK, WALK, 4, D>(ws, m, res, st, stream);
+        case 5: return launch_ladder_k<G, TK, WALK, 5, D>(ws, m, res, st, stream);
+        case 6: return launch_ladder_k<G, TK, WALK, 6, D>(ws, m, res, st, stream);
+        case 7: return launch_ladder_k<G, TK, WALK, 7, D>(ws, m, res, st, stream);
+        case 8: return launch_ladder_k<G, TK, WALK, 8, D>(ws, m, res, st, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 template <int MODE, int TK>
 hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                            uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
                            hipStream_t stream) {
-    if constexpr (MODE == kApplyStack) {
+    if constexpr (MODE == kApplyLadder) {
+        // batch walk at G = 8 (C3, 5 levels at 96-entry runs: 75.6 us against
+        // 84.2 for independent groups at G = 4 and 78.5 at G = 8)
+        return launch_ladder_nf<8, TK, 0>(ws, m, res, st, stream);
+    } else if constexpr (MODE == kApplyStack) {
         // independent lane groups at G = 4 (C3, 5 levels: 108 -> 102 us; 4 levels: equal)
         if (apply_lanes_per_tile(ws.nbins, 3 * TK) <= 4)
             return launch_stack_nf<4, TK, 1>(ws, m, res, st, stream);
         return launch_stack_nf<8, TK>(ws, m, res, st, stream);
-    }
-    switch (apply_lanes_per_tile(ws.nbins, 3 * TK)) {
-        case 4:  // builds: independent lane groups (C2 pass 2 39.5 -> 34.4 us, C4 1.39 -> 1.36 ms)
-            if constexpr (MODE == kApplyBuild)
-                return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
-            else
-                return launch_apply_g<MODE, 4, TK>(ws, m, words, nw32, merge, res, st, stream);
-        case 8: return launch_apply_g<MODE, 8, TK>(ws, m, words, nw32, merge, res, st, stream);
-        case 16: return launch_apply_g<MODE, 16, TK>(ws, m, words, nw32, merge, res, st, stream);
-        default: return launch_apply_g<MODE, 32, TK>(ws, m, words, nw32, merge, res, st, stream);
+    } else {
+        switch (apply_lanes_per_tile(ws.nbins, 3 * TK)) {
+            case 4:  // builds: independent lane groups (C2 pass 2 39.5 -> 34.4 us, C4 1.39 -> 1.36 ms)
+                if constexpr (MODE == kApplyBuild)
+                    return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
+                else
+                    return launch_apply_g<MODE, 4, TK>(ws, m, words, nw32, merge, res, st, stream);
+            case 8: return launch_apply_g<MODE, 8, TK>(ws, m, words, nw32, merge, res, st, stream);
+            case 16: return launch_apply_g<MODE, 16, TK>(ws, m, words, nw32, merge, res, st, stream);
+            default: return launch_apply_g<MODE, 32, TK>(ws, m, words, nw32, merge, res, st, stream);
+        }
     }
 }
 
@@ -1588,6 +1937,27 @@ hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, cons
                                 const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
                                 uint64_t *out, size_t nw, hipStream_t stream) {
     if (ks.n == 0) return hipSuccess;
+    if (st.ladder) {  // plan_ladder's geometry
+        const LadderTable &L = st.lad;
+        if (st.nf < 2 || st.nf > kMaxStack || !mp_max.fast || !mp_max.p2 || !ws.lad_u ||
+            ws.lad_s != L.s || ws.lad_u != L.u || ws.lad_hb != L.hb || ws.nbins != (1u << L.u) ||
+            L.t[0] != mp_max.p2t || L.d != mp_max.p2d || L.s < 7 ||
+            ladder_lds_bytes(L) > kStackMaxBits / 8)
+            return hipErrorInvalidValue;
+        if (L.k < 1 || L.k > (uint32_t)st.nf || (L.k < (uint32_t)st.nf) != (L.bpp != 0) ||
+            (L.bpp != 0 && L.bpp != 4 && L.bpp != 8) || (L.bpp == 4 && st.nf - (int)L.k > 4))
+            return hipErrorInvalidValue;
+        for (int j = 0; j < st.nf; j++)
+            if ((uint64_t)st.mwords[j] * 32 != ((uint64_t)L.d << L.t[j]) || L.t[j] < L.s)
+                return hipErrorInvalidValue;
+        if ((L.rs != 1 && L.rs != 2 && L.rs != 4 && L.rs != 8) || L.base[0] != 0)
+            return hipErrorInvalidValue;
+        hipError_t e = launch_bin<true>(ks, mp_max, ws, slots, stream);
+        if (e != hipSuccess) return e;
+        e = launch_apply<kApplyLadder>(ws, mp_max.m, nullptr, 0, 0, res, st, stream);
+        if (e != hipSuccess) return e;
+        return launch_combine(ws, res, slots, ks.n, out, nw, st, stream);
+    }
     if (st.nf < 1 || st.nf > kMaxStack || !mp_max.fast || ws.seg_bits % 128 != 0 ||
         (uint64_t)ws.nbins * ws.seg_bits != mp_max.m)
         return hipErrorInvalidValue;

@@ -310,3 +310,70 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
     }
     return e == hipSuccess ? 0 : -5;
 }
+
+// Ladder stack (plan_ladder) on the product kernels, tile_keys 4096 or 8192:
+// 0 the whole probe, 1 pass 1, 2 pass 2 (product walk), 5 combine,
+// 20 + G pass 2 at G lanes per tile (independent groups), 30 + G batch walk,
+// 41 / 44 batch walk G = 8 at one / four load groups per wave.
+extern "C" int ubench_ladder(int variant, int tile_keys, const void *keys, size_t n, int nf,
+                             const uint64_t *ms, void *const *words, uint64_t *pos,
+                             uint32_t *runs, uint8_t *res, uint16_t *slots, uint64_t *out,
+                             void *stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
+    PartitionWorkspace ws{};
+    StackTable st{};
+    if (!plan_ladder(ms, nf, device_cu_count(), &st, &ws)) return -34;
+    if (tile_keys) ws.tile_keys = (uint32_t)tile_keys;
+    ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
+    ws.pos = pos;
+    ws.run_rows = runs;
+    ws.run_starts = runs + ws.ntiles * (ws.nbins + 1);
+    st.nf = nf;
+    for (int j = 0; j < nf; j++) {
+        st.words[j] = reinterpret_cast<const uint32_t *>(words[j]);
+        st.mwords[j] = (uint32_t)(ms[j] / 32);
+        st.row[j] = j;
+    }
+    const ModParams mp = make_mod_params(ms[0]);
+    const size_t nw = (n + 63) / 64;
+    const bool big = ws.tile_keys == 2 * kPartTileKeys;
+    constexpr int kB = 2 * (int)kPartTileKeys, kS = (int)kPartTileKeys;
+    hipError_t e = hipSuccess;
+    switch (variant) {
+        case 0: e = launch_probe_stacked(ks, mp, st, ws, res, slots, out, nw, s); break;
+        case 1: e = launch_bin<true>(ks, mp, ws, slots, s); break;
+        case 2: e = launch_apply<kApplyLadder>(ws, ms[0], nullptr, 0, 0, res, st, s); break;
+        case 5: e = launch_combine(ws, res, slots, n, out, nw, st, s); break;
+#define UB_LG(G, W)                                                                        \
+    case 20 + 10 * (1 - W) + G:                                                            \
+        e = big ? launch_ladder_nf<G, kB, W>(ws, ms[0], res, st, s)                         \
+                : launch_ladder_nf<G, kS, W>(ws, ms[0], res, st, s);                        \
+        break;
+        UB_LG(2, 1) UB_LG(4, 1) UB_LG(8, 1) UB_LG(4, 0) UB_LG(8, 0) UB_LG(16, 0)
+#undef UB_LG
+        case 41:  // batch walk G = 8, one load group in flight per wave
+            e = big ? launch_ladder_nf<8, kB, 0, 1>(ws, ms[0], res, st, s)
+                    : launch_ladder_nf<8, kS, 0, 1>(ws, ms[0], res, st, s);
+            break;
+        case 44:  // batch walk G = 8, four load groups
+            e = big ? launch_ladder_nf<8, kB, 0, 4>(ws, ms[0], res, st, s)
+                    : launch_ladder_nf<8, kS, 0, 4>(ws, ms[0], res, st, s);
+            break;
+        default: return -22;
+    }
+    return e == hipSuccess ? 0 : -5;
+}
+
+extern "C" int ubench_ladder_geometry(int nf, const uint64_t *ms, uint64_t *out6) {
+    PartitionWorkspace ws{};
+    StackTable st{};
+    if (!plan_ladder(ms, nf, device_cu_count(), &st, &ws)) return -34;
+    out6[0] = ws.nbins;
+    out6[1] = st.lad.s;
+    out6[2] = st.lad.hb;
+    out6[3] = ladder_lds_bytes(st.lad);
+    out6[4] = st.lad.k;
+    out6[5] = st.lad.bpp;
+    return 0;
+}

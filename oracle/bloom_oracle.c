@@ -9,7 +9,7 @@
  * load this library.  Nothing in the product (cs265-lsm-tree_amd/) links it.
  *
  * Pinning: the reference needs boost::dynamic_bitset, which is not installed
- * in this image, so the reference itself is unbuildable here (DESIGN.md §3).
+ * in this image, so the reference itself is unbuildable here (DESIGN.md §2).
  * This restatement is pinned by the known-answer table and the C2/C3 popcount
  * and hit-count vectors recorded from the compiled reference in SURVEY.md
  * §8a/§8c (tests/golden/), and by the reference's own golden test test-6

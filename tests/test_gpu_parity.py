@@ -294,6 +294,31 @@ def test_stacked_probe_matches_oracle(coracle, ms):
     _stack_case(coracle, ms, probe)
 
 
+@pytest.mark.parametrize("ms", [
+    [655_360 * 4**i for i in range(5)],           # C3's levels: d = 5, t = 17..25
+    [3 * 2**(16 + 2 * i) for i in range(4)],      # 12 bits/key levels: d = 3
+    [5 * 2**25, 5 * 2**21, 5 * 2**20],            # uneven spacing (fanout 16, then 2)
+    [5 * 2**22, 5 * 2**22, 5 * 2**20],            # a repeated size
+    [5 * 2**(14 + 2 * i) for i in range(6)],      # six members, 2 KiB blocks
+    [17 * 2**24, 17 * 2**20],                     # d = 17
+    [5 * 2**20, 3 * 2**20, 5 * 2**18],            # two odd parts: not a ladder (segment stack)
+], ids=["c3", "d3", "uneven", "repeat", "six", "d17", "not_ladder"])
+def test_ladder_stack_matches_oracle(coracle, ms):
+    """Levels d << t_j probed in one ladder pass (bins = hash bits, the
+    members' blocks staged per bin); every member's rows against the oracle."""
+    probe = rand_keys(300_001, 83)
+    _stack_case(coracle, ms, probe, seed=11)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 8191, 8193])
+def test_ladder_stack_tiny_ragged_and_strided(coracle, n):
+    """A ladder over batches smaller than one 8192-key tile or one tile plus
+    one key, and entry_t keys at stride 8."""
+    ms = [655_360 * 4**i for i in range(4)]
+    _stack_case(coracle, ms, rand_keys(n, 90 + n), seed=3)
+    _stack_case(coracle, ms, rand_keys(n, 91 + n), stride=8, seed=4)
+
+
 def test_stacked_probe_auto_and_strided(coracle):
     """AUTO stacks a divisible group at >= 2^18 keys; AoS entry_t keys."""
     ms = [655_360 * 4**i for i in range(5)]

@@ -35,10 +35,13 @@ for s in ${STEPS//,/ }; do
     ub_part_c5) run ub_part_c5 300 python tools/ubench.py part_c5 || exit 1 ;;
     ub_part_c4) run ub_part_c4 300 python tools/ubench.py part_c4 || exit 1 ;;
     ub_stack) run ub_stack 300 python tools/ubench.py stack || exit 1 ;;
+    ub_ladder) run ub_ladder 300 python tools/ubench.py ladder || exit 1 ;;
     ub_p1ab) run ub_p1ab 300 python tools/ubench.py p1ab || exit 1 ;;
     sq_part) run sq_part_a 150 timeout -s KILL 140 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d "$OUT/sq_part_a" -o pmc --output-format csv -- python tools/ubench.py part || exit 1
              run sq_part_b 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace -d "$OUT/sq_part_b" -o pmc --output-format csv -- python tools/ubench.py part || exit 1
              run sq_part_c 150 timeout -s KILL 140 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d "$OUT/sq_part_c" -o pmc --output-format csv -- python tools/ubench.py part || exit 1 ;;
+    sq_c3) run sq_c3_a 150 timeout -s KILL 140 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d "$OUT/sq_c3_a" -o pmc --output-format csv -- python tools/probe_prof.py auto 10 || exit 1
+           run sq_c3_b 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace -d "$OUT/sq_c3_b" -o pmc --output-format csv -- python tools/probe_prof.py auto 10 || exit 1 ;;
     bench_c5) run bench_c5 400 python bench.py --workload c5 --steps 20 --warmup 3 --no-extras --no-cpu-baseline || exit 1 ;;
     stats_c2) run stats_c2 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c2" -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline --prewarm-s 0 || exit 1 ;;
     stats_c3) run stats_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3" -o run --output-format csv -- python tools/probe_prof.py auto 30 || exit 1 ;;

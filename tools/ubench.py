@@ -198,6 +198,88 @@ def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
                           "us": round(a.elapsed_time(b) / 20 * 1e3, 1)}), flush=True)
 
 
+LIB.ubench_ladder.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_void_p] * 6
+LIB.ubench_ladder.restype = ctypes.c_int
+LIB.ubench_ladder_geometry.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+LIB.ubench_ladder_geometry.restype = ctypes.c_int
+
+
+def ladder_ablation(levels_sel=(0, 1, 2, 3, 4), reps=20):
+    """The C3 probe as a ladder stack (bins = hash bits), by phase, per tile
+    size and pass-2 lane count, each checked against the segment stack's
+    answers (ubench_stack variant 0, the round-2 product kind)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
+    import bloomhip as bh
+    from bloomhip import workloads as W
+    gets, levels = W.c3()
+    filters, ms = [], []
+    for lvl, keys, m in sorted(levels, key=lambda x: -x[2]):
+        if lvl in levels_sel:
+            f = bh.BloomFilter(m)
+            f.set_batch(keys)
+            filters.append(f)
+            ms.append(m)
+    nf = len(ms)
+    msa = np.array(ms, dtype=np.uint64)
+    wp = (ctypes.c_void_p * nf)(*[f.device_words_ptr() for f in filters])
+    geo = np.zeros(6, dtype=np.uint64)
+    assert LIB.ubench_ladder_geometry(nf, msa.ctypes.data, geo.ctypes.data) == 0
+    n = gets.size
+    ntiles = (n + 4095) // 4096
+    dk = torch.from_numpy(gets).cuda()
+    pos = torch.empty(ntiles * 4096, dtype=torch.int64, device="cuda")
+    runs = torch.empty(2 * ntiles * 4097, dtype=torch.int32, device="cuda")
+    res = torch.empty(ntiles * 4096 * 3, dtype=torch.uint8, device="cuda")
+    slots = torch.empty(ntiles * 4096 * 3, dtype=torch.int16, device="cuda")
+    out = torch.empty(nf * ((n + 63) // 64), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream()
+    nb, sb = ctypes.c_uint64(), ctypes.c_uint64()
+    assert LIB.ubench_stack_geometry(nf, msa.ctypes.data, ctypes.byref(nb), ctypes.byref(sb)) == 0
+    assert LIB.ubench_stack(0, dk.data_ptr(), n, nf, msa.ctypes.data, wp, pos.data_ptr(),
+                            runs.data_ptr(), res.data_ptr(), slots.data_ptr(), out.data_ptr(),
+                            s.cuda_stream) == 0
+    torch.cuda.synchronize()
+    ref = out.clone()
+
+    def run(v, tk):
+        return LIB.ubench_ladder(v, tk, dk.data_ptr(), n, nf, msa.ctypes.data, wp, pos.data_ptr(),
+                                 runs.data_ptr(), res.data_ptr(), slots.data_ptr(),
+                                 out.data_ptr(), s.cuda_stream)
+
+    def stack(v):
+        return LIB.ubench_stack(v, dk.data_ptr(), n, nf, msa.ctypes.data, wp, pos.data_ptr(),
+                                runs.data_ptr(), res.data_ptr(), slots.data_ptr(), out.data_ptr(),
+                                s.cuda_stream)
+    for tk in (8192, 4096):
+        for v in (2, 22, 24, 28, 34, 38, 46, 41, 44):
+            out.zero_()
+            ok = run(1, tk) == 0 and run(v, tk) == 0 and run(5, tk) == 0
+            torch.cuda.synchronize()
+            print(json.dumps({"check": f"ladder tk={tk} pass-2 variant {v} == segment stack",
+                              "ok": bool(ok and torch.equal(ref, out))}), flush=True)
+    names = {0: "all three", 1: "pass 1 (+slots)", 2: "pass 2 (product)", 5: "combine",
+             22: "pass 2 G=2", 24: "pass 2 G=4", 28: "pass 2 G=8", 34: "pass 2 batch G=4",
+             38: "pass 2 batch G=8", 46: "pass 2 batch G=16", 41: "pass 2 batch G=8 d=1",
+             44: "pass 2 batch G=8 d=4"}
+    _prewarm(lambda v: run(0, 8192), 0)
+    for rnd in range(2):
+        t = _events(lambda: stack(0), reps)
+        print(json.dumps({"op": "segment stack (round 2 kind)", "levels": list(levels_sel),
+                          "round": rnd, "us": round(t * 1e3, 1)}), flush=True)
+        for tk in (8192, 4096):
+            for v in names:
+                if run(v, tk) != 0:
+                    continue
+                t = _events(lambda: run(v, tk), reps)
+                print(json.dumps({"op": "ladder stack", "levels": list(levels_sel), "tile_keys": tk,
+                                  "nbins": int(geo[0]), "s": int(geo[1]), "hb": int(geo[2]),
+                                  "lds_bytes": int(geo[3]), "k": int(geo[4]), "bpp": int(geo[5]),
+                                  "phase": names[v], "round": rnd,
+                                  "us": round(t * 1e3, 1)}), flush=True)
+
+
 def mixed():
     """Can LDS atomics and VALU hashing overlap on a CU?  Some of 16 waves
     hash, the rest do random ds_add_rtn: time both together vs each alone."""
@@ -217,6 +299,9 @@ def main():
     torch.cuda.set_device(0)
     if len(sys.argv) > 1 and sys.argv[1] == "mixed":
         return mixed()
+    if len(sys.argv) > 1 and sys.argv[1] == "ladder":
+        ladder_ablation()
+        return ladder_ablation((0, 1, 2, 3))
     if len(sys.argv) > 1 and sys.argv[1] == "stack":
         stack_ablation()
         return stack_ablation((0, 1, 2, 3))
