@@ -201,6 +201,19 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     }
         UB_P2(5001, 512, 511, 4, 2) UB_P2(5003, 512, 511, 6, 3)
 #undef UB_P2
+        // pass 2 at G lanes per tile, W = 1 independent groups / 0 batch walk
+#define UB_P2G(G, W)                                                                              \
+    case 2000 + 10 * G + W: {                                                                    \
+        const uint64_t nw32 = ((m + 63) / 64) * 2;                                               \
+        e = ws.tile_keys == 2 * kPartTileKeys                                                   \
+                ? launch_apply_g<kApplyBuild, G, 2 * (int)kPartTileKeys, kApplyDepth, W>(        \
+                      ws, m, words, nw32, 0, nullptr, StackTable{}, s)                           \
+                : launch_apply_g<kApplyBuild, G, (int)kPartTileKeys, kApplyDepth, W>(            \
+                      ws, m, words, nw32, 0, nullptr, StackTable{}, s);                          \
+        break;                                                                                   \
+    }
+        UB_P2G(1, 1) UB_P2G(2, 1) UB_P2G(4, 1) UB_P2G(8, 1) UB_P2G(2, 0) UB_P2G(4, 0)
+#undef UB_P2G
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

@@ -35,6 +35,7 @@ for s in ${STEPS//,/ }; do
     ub_part_c5) run ub_part_c5 300 python tools/ubench.py part_c5 || exit 1 ;;
     ub_part_c4) run ub_part_c4 300 python tools/ubench.py part_c4 || exit 1 ;;
     ub_stack) run ub_stack 300 python tools/ubench.py stack || exit 1 ;;
+    pcie) run pcie 120 python tools/pcie_probe.py || exit 1 ;;
     ub_ladder) run ub_ladder 300 python tools/ubench.py ladder || exit 1 ;;
     ub_p1ab) run ub_p1ab 300 python tools/ubench.py p1ab || exit 1 ;;
     sq_part) run sq_part_a 150 timeout -s KILL 140 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d "$OUT/sq_part_a" -o pmc --output-format csv -- python tools/ubench.py part || exit 1

@@ -88,14 +88,25 @@ def _prewarm(run, v, secs=0.5):
 
 def part_phases(n=16_777_216, bpe=10.0, reps=50):
     """The product's partition build by pass (pass 2 timed over pass 1's
-    output), two rounds."""
+    output), and pass 2 at other lane counts / walks, two rounds."""
     run, words, geo = _part_setup(n, bpe)
     assert run(0) == 0 and run(1) == 0
     torch.cuda.synchronize()
-    _prewarm(run, 0)
+    ref = words.clone()
     names = {0: "pass 1 (product)", 1: "pass 2 (product)"}
+    for g, w in ((1, 1), (2, 1), (4, 1), (8, 1), (2, 0), (4, 0)):
+        v = 2000 + 10 * g + w
+        words.zero_()
+        if run(v) != 0:
+            continue
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(ref, words))
+        print(json.dumps({"check": f"pass-2 variant {v} bitmap == product", "ok": ok}), flush=True)
+        if ok:
+            names[v] = f"pass 2 G={g} {'indep' if w else 'batch'}"
+    _prewarm(run, 0)
     for rnd in range(2):
-        for v in (0, 1):
+        for v in names:
             ms = _events(lambda: run(v), reps)
             print(json.dumps({"op": "partition build", **geo, "phase": names[v], "round": rnd,
                               "us": round(ms * 1e3, 1)}), flush=True)
