@@ -94,8 +94,8 @@ struct SegMap {
 
 struct PartitionWorkspace {
     uint64_t *pos;         // [ntiles * tile_keys] packed sorted entries (3 per u64)
-    uint32_t *run_rows;    // [ntiles * (nbins + 1)], pass-1 run starts, tile-major
-    uint32_t *run_starts;  // [(nbins + 1) * ntiles], the same segment-major (pass 2)
+    uint32_t *run_rows;    // [ntiles * nbins], pass-1 runs (start | end << 16), tile-major
+    uint32_t *run_starts;  // [nbins * ntiles], the same segment-major (pass 2)
     size_t ntiles;
     size_t nbins;          // segments
     uint32_t sub_shift;    // q = pos >> sub_shift

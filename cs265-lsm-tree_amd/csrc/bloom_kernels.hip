@@ -135,9 +135,9 @@ __global__ void __launch_bounds__(kBlock) k_build_lds(KeySpan ks, ModParams mp,
 // gives each its rank in its segment, a scan gives the segment offsets) and
 // the sorted tile goes out packed: the low kEntryBits bits of each position,
 // three per u64, 8 B per key-hash triple instead of 12.
-// Column `tile` of the segment-major run table gets where each segment's run
-// starts (nbins + 1 entries), so segment b's run of this tile is
-// [runs[b][tile], runs[b+1][tile]).  No global atomics.
+// Column `tile` of the segment-major run table gets each segment's run of
+// the tile, [start, end) in entries packed start | end << 16 (one u32 per
+// (tile, segment): pass 2 reads the table once).  No global atomics.
 //
 // The next tile's keys are loaded while the current tile is sorted, and the
 // workgroup barriers wait only for LDS (lgkmcnt), so the sorted tile's
@@ -277,10 +277,10 @@ __device__ __forceinline__ uint32_t seg_of(P p, const SegMap &sm) {
 constexpr uint32_t kBinShift = 19;  // 8192 segments << 19 < 2^32
 
 // Outputs: pos_out[tile * kTileKeys ..] (u64), the tile's entries sorted by
-// segment, packed three per u64; where segment b's run of the tile starts
-// (b = 0..nbins): COLS = true: straight into the segment-major table
+// segment, packed three per u64; segment b's run of the tile (start | end
+// << 16, b = 0..nbins-1): COLS = true: straight into the segment-major table
 // runs[b * ntiles + tile]; COLS = false: into the tile-major
-// runs[tile * (nbins + 1) + b], for k_runs_transpose (large tables).
+// runs[tile * nbins + b], for k_runs_transpose (large tables).
 constexpr int kModFast = 0, kModWide = 1, kModP2 = 2, kModLadder = 3;
 
 template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4>
@@ -292,7 +292,8 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
     constexpr int kTilePos = 3 * kTileKeys;
     constexpr int kMaxB = MAXB ? MAXB : TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
     constexpr int kScanPer = (kMaxB + 1 + TB - 1) / TB;  // scan entries per thread, at most
-    static_assert(4 * kTilePos <= (1 << 17) && ((uint64_t)(kMaxB - 1) << kBinShift) < (1ull << 32),
+    static_assert(4 * kTilePos <= (1 << 17) && kTilePos < (1 << 16) &&
+                      ((uint64_t)(kMaxB - 1) << kBinShift) < (1ull << 32),
                   "packed rank fields (bin nbins, never incremented, may wrap to 0)");
     // static LDS even for the 96 KiB of an 8192-key tile (gfx950 takes it);
     // dynamic LDS or a pointer to it made the compiler spill registers here
@@ -397,11 +398,15 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                 if (q < per && b <= nb) {
                     // biased by -(b << kBinShift): bin + rank value = byte slot
                     s_hist[b] = run - ((uint32_t)b << kBinShift);
-                    // where segment b's run starts (entry index), straight
+                    // segment b's run of this tile, [start, end) in entries,
+                    // packed start | end << 16 (both < 3 * 8192), straight
                     // from the scan's registers: segment-major column or
                     // tile-major row
-                    if constexpr (COLS) runs[(size_t)b * ntiles + tile] = run >> 2;
-                    else runs[tile * (size_t)(nb + 1) + b] = run >> 2;
+                    const uint32_t pk = (run >> 2) | (((run + local[q]) >> 2) << 16);
+                    if (b < nb) {
+                        if constexpr (COLS) runs[(size_t)b * ntiles + tile] = pk;
+                        else runs[tile * (size_t)nb + b] = pk;
+                    }
                     run += local[q];
                 }
             }
@@ -491,7 +496,7 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
 }
 
 // ---------------------------------------------------------------------------
-// run-start transpose: pass 1 writes one row of nbins + 1 run starts per tile
+// run-table transpose: pass 1 writes one row of nbins packed runs per tile
 // (contiguous, cheap); pass 2 wants, per segment, its run bounds of all tiles
 // contiguous.  A 64 x 64 LDS-tiled transpose: 256-B coalesced reads and
 // writes, the LDS tile padded one word per row against bank conflicts.
@@ -742,16 +747,17 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const int tl = lane / G;                    // this lane's tile in a load group
     const int nbatch = (ntiles + kBatchTiles - 1) / kBatchTiles;
 
-    auto bounds = [&](int j, uint2 (&r)[DEPTH]) {
+    // Run bounds travel packed (start | end << 16) until they are used: a
+    // decode right after the prefetching load makes the compiler wait for
+    // it there, i.e. for every load issued before it, the entry-vector
+    // prefetch included (that wait made the packed table slower than two
+    // u32 columns: C2 pass 2 36 -> 41 us, C4 1.22 -> 1.56 ms).
+    auto dec = [](uint32_t pk) { return make_uint2(pk & 0xFFFFu, pk >> 16); };
+    auto bounds = [&](int j, uint32_t (&r)[DEPTH]) {
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) {
             const int t = j * kBatchTiles + d * kTPI + tl;
-            if (t < ntiles) {
-                r[d] = make_uint2(run_starts[(size_t)b * ntiles + t],
-                                  run_starts[(size_t)(b + 1) * ntiles + t]);
-            } else {
-                r[d] = make_uint2(0, 0);
-            }
+            r[d] = t < ntiles ? run_starts[(size_t)b * ntiles + t] : 0u;
         }
     };
     // Vector vi of tile t; lanes past the tile's last vector load that one
@@ -896,48 +902,52 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         // one is applied, and the next tile's run bounds one tile ahead.
         constexpr int kGroupsPerWave = 64 / G;
         const int Q = kGroupsPerWave * (BLOCK / 64);
-        auto bnd = [&](int tt) -> uint2 {
-            return tt < ntiles ? make_uint2(run_starts[(size_t)b * ntiles + tt],
-                                            run_starts[(size_t)(b + 1) * ntiles + tt])
-                               : make_uint2(0, 0);
+        auto bnd = [&](int tt) -> uint32_t {  // packed; 0 = empty past the end
+            return tt < ntiles ? run_starts[(size_t)b * ntiles + tt] : 0u;
         };
+        // the current and the next tile's bounds both stay packed (a decode
+        // of the next one as it becomes current would sit between its load
+        // and its register: a copy, hence a wait)
         int t = wave * kGroupsPerWave + tl;
-        uint2 r = bnd(t), rn = bnd(t + Q);
-        uint32_t vb = r.x / 6u;  // the group's step base (vector index)
-        // state after this step: advance within the run or to the next tile
-        auto step = [&](int &tt, uint2 &rr, uint2 &rrn, uint32_t &vvb) {
-            vvb += G;
-            if (6 * vvb >= rr.y) {
-                tt += Q;
-                rr = rrn;
-                vvb = rr.x / 6u;
-                rrn = bnd(tt + Q);
-            }
-        };
+        uint32_t r = bnd(t), rn = bnd(t + Q);
+        uint32_t vb = (r & 0xFFFFu) / 6u;  // the group's step base (vector index)
         uint4 v = load(min(t, ntiles - 1), vb + sub);
         while (__ballot(t < ntiles) != 0) {
+            // state after this step: advance within the run or to the next
+            // tile.  On a tile change the new lookahead bounds are loaded
+            // straight into their loop register, before the next step's
+            // vector, so the wait before the apply (vmcnt 1) leaves only that
+            // vector in flight
             int t2 = t;
-            uint2 r2 = r, rn2 = rn;
-            uint32_t vb2 = vb;
-            step(t2, r2, rn2, vb2);
+            uint32_t r2 = r, vb2 = vb + G;
+            const bool adv = 6 * vb2 >= (r >> 16);
+            if (adv) {
+                t2 += Q;
+                r2 = rn;
+                vb2 = (r2 & 0xFFFFu) / 6u;
+            }
+            uint32_t rn2 = rn;
+            if (adv) rn2 = bnd(t2 + Q);
             const uint4 v2 = load(min(t2, ntiles - 1), vb2 + sub);
-            if (t < ntiles && 6 * vb < r.y) apply6(v, t, vb + sub, r);
+            if (t < ntiles && 6 * vb < (r >> 16)) apply6(v, t, vb + sub, dec(r));
             t = t2; r = r2; rn = rn2; vb = vb2; v = v2;
         }
     } else {
-    uint2 r[DEPTH];
-    if (wave < nbatch) bounds(wave, r);
+    uint32_t rp[DEPTH];  // this batch's bounds, packed
+    if (wave < nbatch) bounds(wave, rp);
     for (int j = wave; j < nbatch; j += (BLOCK / 64)) {
         int t[DEPTH];
         uint32_t vi[DEPTH];
         uint4 v[DEPTH];
+        uint2 r[DEPTH];
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) {
+            r[d] = dec(rp[d]);
             t[d] = min(j * kBatchTiles + d * kTPI + tl, ntiles - 1);
             vi[d] = r[d].x / 6u + sub;
             v[d] = load(t[d], vi[d]);
         }
-        uint2 rn[DEPTH];
+        uint32_t rn[DEPTH];
         const int jn = j + (BLOCK / 64);
         if (jn < nbatch) bounds(jn, rn);
 #pragma unroll
@@ -948,7 +958,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                 apply6(load(t[d], vn), t[d], vn, r[d]);
         }
 #pragma unroll
-        for (int d = 0; d < DEPTH; d++) r[d] = rn[d];
+        for (int d = 0; d < DEPTH; d++) rp[d] = rn[d];
     }
     }
     if constexpr (PROBE) return;
@@ -1638,7 +1648,7 @@ bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWo
 }
 
 hipError_t launch_runs_transpose(const PartitionWorkspace &ws, hipStream_t stream) {
-    const int width = (int)ws.nbins + 1;
+    const int width = (int)ws.nbins;
     const dim3 grid((unsigned)((width + kTransposeTile - 1) / kTransposeTile),
                     (unsigned)((ws.ntiles + kTransposeTile - 1) / kTransposeTile));
     if (grid.y > 65535u) return hipErrorInvalidValue;  // > 2^28 keys per batch
@@ -1648,7 +1658,7 @@ hipError_t launch_runs_transpose(const PartitionWorkspace &ws, hipStream_t strea
 }
 
 bool runs_as_columns(const PartitionWorkspace &ws) {
-    return ws.ntiles * (ws.nbins + 1) * 4 <= kColumnTableMaxBytes;
+    return ws.ntiles * ws.nbins * 4 <= kColumnTableMaxBytes;
 }
 
 // One pass-1 launch: MAXB is the histogram capacity the kernel is compiled

@@ -19,7 +19,9 @@ d = json.loads(next(l for l in open(sys.argv[1]) if l.startswith("{")))
 k = d["roofline"].get("profiled_kernel_ms", {})
 x = {kk: round(v * 1e3, 1) for kk, v in k.items()}
 p = d.get("probe_c3", {})
-print(sys.argv[2], sys.argv[3], d["value"], d["ms_per_step"], x, "probe_c3", p.get("kernel_ms"))
+c4 = d.get("c4_build", {})
+print(sys.argv[2], sys.argv[3], d["value"], d["ms_per_step"], x, "probe_c3", p.get("kernel_ms"),
+      "c4", c4.get("gkeys_s"), c4.get("kernels"), "route", d.get("route_c3", {}).get("wall_ms"))
 PY
   done
 done
