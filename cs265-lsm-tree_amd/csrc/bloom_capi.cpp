@@ -350,9 +350,10 @@ int partition_buffers(Workspace *w, size_t n, hipStream_t s, PartitionWorkspace 
 // Geometry of a partition pass over n keys for filter size m, with the
 // position/run buffers of `w` grown to fit.
 int partition_workspace(Workspace *w, uint64_t m, size_t n, hipStream_t s,
-                        PartitionWorkspace *out) {
+                        PartitionWorkspace *out, bool build = false) {
     PartitionWorkspace ws{};
-    if (!plan_segments(m, device_cu_count(), &ws)) return BLOOMHIP_ERANGE;
+    if (!(build ? plan_build(m, device_cu_count(), &ws) : plan_segments(m, device_cu_count(), &ws)))
+        return BLOOMHIP_ERANGE;
     *out = ws;
     return partition_buffers(w, n, s, out);
 }
@@ -404,7 +405,7 @@ int run_partition(bloomhip_filter *f, const KeySpan &ks, hipStream_t s) {
     const std::shared_ptr<Workspace> w = workspace_for(f->device, s);
     std::lock_guard<std::recursive_mutex> lk(w->mu);
     PartitionWorkspace ws{};
-    int rc = partition_workspace(w.get(), f->m, ks.n, s, &ws);
+    int rc = partition_workspace(w.get(), f->m, ks.n, s, &ws, /*build=*/true);
     if (rc) return rc;
     hipError_t e = timed(f, SLOT_PART_BIN, s, [&] { return launch_part_bin(ks, f->mp, ws, s); });
     if (e != hipSuccess) return fail_hip(e, "k_part_bin");

@@ -141,6 +141,15 @@ int device_cu_count();
 // partition path does not apply (more than kPartMaxBinsBig segments of at
 // most 160 KiB: m above about 2^33.3 bits).
 bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws);
+// Build geometry: plan_segments, then, when m = d << t (the p2 form) and the
+// segment count is a power of two 2^u, the same bins taken as hash bits
+// [t - u, t) (a one-member ladder, kernels.h LadderTable): bin b holds the d
+// blocks a << t | b << s (s = t - u) of 2^s bits, its entry is a << s | the
+// hash's low s bits, so pass 1 takes the bin with one bit-field extract
+// instead of a shift and multiply-high and pass 2 addresses the image with
+// the entry itself.  C2 (5 << 25: 256 bins of 80 KiB) and C5 (5 << 27: 512
+// of 160 KiB) take it; C4 (3 << 30, 2,458 segments) keeps segments.
+bool plan_build(uint64_t m, int ncu, PartitionWorkspace *ws);
 
 // Probe: filters up to this size are gathered directly; larger ones use the
 // partitioned probe when the batch has at least kProbePartitionMinKeys keys.

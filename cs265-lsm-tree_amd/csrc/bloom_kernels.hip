@@ -175,6 +175,13 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, S sh, uint32_t b) {
     return r;
 }
 
+// (a << s) | b in one instruction, s in an SGPR.
+__device__ __forceinline__ uint32_t lshl_or_s(uint32_t a, uint32_t sh, uint32_t b) {
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(sh), "v"(b));
+    return r;
+}
+
 // Workgroup barrier that waits for this wave's LDS operations only.
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -281,7 +288,7 @@ constexpr uint32_t kBinShift = 19;  // 8192 segments << 19 < 2^32
 // << 16, b = 0..nbins-1): COLS = true: straight into the segment-major table
 // runs[b * ntiles + tile]; COLS = false: into the tile-major
 // runs[tile * nbins + b], for k_runs_transpose (large tables).
-constexpr int kModFast = 0, kModWide = 1, kModP2 = 2, kModLadder = 3;
+constexpr int kModFast = 0, kModWide = 1, kModP2 = 2, kModLadder = 3, kModLadder0 = 4;
 
 template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4>
 __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
@@ -348,6 +355,23 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                         const uint32_t ehi =
                             (a << sm.lad_hb) + __builtin_amdgcn_ubfe(xl, sm.scaled_shift, sm.lad_hb);
                         ent[3 * j + h] = (ehi << sm.shift) | __builtin_amdgcn_ubfe(xl, 0, sm.shift);
+                    } else if constexpr (MK == kModLadder0) {
+                        // one-member ladder (plan_build): bin = hash bits
+                        // [s, t), entry = a << s | bits [0, s)
+                        const uint32_t xl = (uint32_t)raw;
+                        if constexpr (MINW >= 6) {
+                            // at the 80-VGPR cap of three workgroups per CU
+                            // the plain form spilled 50 VGPRs
+                            const uint32_t lo = __builtin_amdgcn_ubfe(xl, 0, sm.shift);
+                            b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
+                            ent[3 * j + h] = lshl_or_s(mod_p2_hi(raw, mp), sm.shift, lo);
+                        } else {
+                            // (C5's pass 1: 229 us, against 256 for the pinned
+                            // form above and for segments)
+                            const uint32_t a = mod_p2_hi(raw, mp);
+                            b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
+                            ent[3 * j + h] = (a << sm.shift) | __builtin_amdgcn_ubfe(xl, 0, sm.shift);
+                        }
                     } else if constexpr (MK == kModP2) {
                         const uint32_t xl = (uint32_t)raw;
                         const uint32_t r = mod_p2_hi(raw, mp);
@@ -568,6 +592,10 @@ inline int apply_lanes_per_tile(size_t nbins, size_t tile_pos = kPartTilePos) {
 // run bounds are loaded while the current one is applied, and the rare tile
 // whose run outlasts the first step is finished by a wave-uniform loop.
 constexpr int kApplyBuild = 0, kApplyProbe = 1, kApplyStack = 2, kApplyLadder = 3;
+// kApplyBuildL: a build on plan_build's one-member ladder (bins = hash bits):
+// the entry is the image offset itself, and the image's d blocks go to
+// a << t | b << s (StackTable::lad's s, t[0], d).
+constexpr int kApplyBuildL = 4;
 
 template <int MODE, int G, int TILE_KEYS, int BLOCK = kApplyBlock, int DEPTH = kApplyDepth,
           int WALK = 0, int NF = 0, int LK = 0>
@@ -575,7 +603,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     const uint64_t *__restrict__ pos, const uint32_t *__restrict__ run_starts, int ntiles,
     int nbins, uint32_t seg_bits, uint64_t m, uint32_t *__restrict__ words, uint64_t nw32,
     int merge_existing, uint8_t *__restrict__ res, StackTable st) {
-    constexpr bool PROBE = MODE != kApplyBuild;
+    constexpr bool PROBE = MODE != kApplyBuild && MODE != kApplyBuildL;
     static_assert(G >= 1 && G <= 64 && (64 % G) == 0, "G lanes per tile");
     constexpr int kTilePos = 3 * TILE_KEYS;
     constexpr int kTPI = 64 / G;                 // tiles per load instruction
@@ -788,7 +816,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             const uint32_t vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
 #pragma unroll
             for (int k = 0; k < 6; k++) {
-                const uint32_t d = e[k] - base21;
+                const uint32_t d = MODE == kApplyBuildL ? e[k] : e[k] - base21;
                 const uint32_t addr = (d >> 3) & ((kEntryMask >> 3) & ~3u);
                 const uint32_t bit = __builtin_amdgcn_ubfe(vm, k, 1) << (d & 31);
                 __attribute__((address_space(3))) uint32_t *w =
@@ -963,6 +991,25 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     }
     if constexpr (PROBE) return;
     __syncthreads();
+
+    if constexpr (MODE == kApplyBuildL) {
+        // block a of the image (2^s bits) is the bitmap's bits a << t | b << s
+        const uint32_t ls = st.lad.s, lt = st.lad.t[0];
+        const uint32_t vpb = 1u << (ls - 7);  // 16-B vectors per block
+        const uint4 *seg4 = reinterpret_cast<const uint4 *>(seg);
+        uint4 *w4 = reinterpret_cast<uint4 *>(words);
+        for (uint32_t q = threadIdx.x; q < st.lad.d * vpb; q += BLOCK) {
+            const uint32_t a = q >> (ls - 7), i = q & (vpb - 1u);
+            uint4 *dq = w4 + (((size_t)a << (lt - 7)) + ((size_t)b << (ls - 7)) + i);
+            uint4 v = seg4[q];
+            if (merge_existing) {
+                const uint4 o = *dq;
+                v.x |= o.x; v.y |= o.y; v.z |= o.z; v.w |= o.w;
+            }
+            *dq = v;
+        }
+        return;
+    }
 
     uint32_t *dst = words + w0;
     if (nseg == (int)seg_words) {  // seg_words % 4 == 0 and w0 is 16-B aligned
@@ -1513,6 +1560,25 @@ bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
     return true;
 }
 
+bool plan_build(uint64_t m, int ncu, PartitionWorkspace *ws) {
+    if (!plan_segments(m, ncu, ws)) return false;
+    uint32_t d = 0, t = 0;
+    if (!p2_form(m, &d, &t)) return true;
+    uint32_t u = 0;
+    while (((size_t)1 << u) < ws->nbins) u++;
+    if (((size_t)1 << u) != ws->nbins || t < u + 7) return true;
+    const uint32_t sl = t - u;
+    uint32_t dbits = 0;
+    while ((1u << dbits) < d) dbits++;
+    if (sl + dbits > kEntryBits || ((uint64_t)d << sl) > kStackMaxBits || ((d << sl) % 1024) != 0)
+        return true;
+    ws->lad_s = sl;
+    ws->lad_u = u;
+    ws->lad_hb = 0;
+    ws->seg_bits = d << sl;  // the bin's image: d blocks of 2^s bits
+    return true;
+}
+
 bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
                 PartitionWorkspace *ws) {
     if (m_max == 0 || m_max > 0xFFFFFFFFull || nf < 1 || nf > kMaxStack || gcd_m == 0 ||
@@ -1736,7 +1802,14 @@ hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const Partition
         if (!mp.fast || !mp.p2 || sm.shift + sm.lad_u + sm.lad_hb != mp.p2t)
             return hipErrorInvalidValue;
         sm.scaled_shift = sm.shift + sm.lad_u;
-        if (ks.layout == KEYS_PACKED)
+        if (sm.lad_hb == 0 && !SLOTS) {  // plan_build's one-member ladder
+            if (ks.layout == KEYS_PACKED)
+                bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModLadder0>(ks, mp, ws, runs, sm, cols, slots, stream);
+            else if (entry16)
+                bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModLadder0>(ks, mp, ws, runs, sm, cols, slots, stream);
+            else
+                bin_launch<KEYS_STRIDED, SLOTS, TB, kModLadder0, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
+        } else if (ks.layout == KEYS_PACKED)
             bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModLadder>(ks, mp, ws, runs, sm, cols, slots, stream);
         else if (entry16)
             bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModLadder>(ks, mp, ws, runs, sm, cols, slots, stream);
@@ -1884,7 +1957,7 @@ hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *w
     } else {
         switch (apply_lanes_per_tile(ws.nbins, 3 * TK)) {
             case 4:  // builds: independent lane groups (C2 pass 2 39.5 -> 34.4 us, C4 1.39 -> 1.36 ms)
-                if constexpr (MODE == kApplyBuild)
+                if constexpr (MODE == kApplyBuild || MODE == kApplyBuildL)
                     return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
                 else
                     return launch_apply_g<MODE, 4, TK>(ws, m, words, nw32, merge, res, st, stream);
@@ -1924,6 +1997,18 @@ hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const Partiti
                              int merge_existing, hipStream_t stream) {
     if (ws.ntiles == 0) return hipSuccess;
     const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
+    if (ws.lad_u) {  // plan_build's one-member ladder
+        if (!mp.p2 || ws.lad_hb != 0 || ws.lad_s + ws.lad_u != mp.p2t || ws.lad_s < 7 ||
+            ws.seg_bits != (mp.p2d << ws.lad_s) || ws.nbins != ((size_t)1 << ws.lad_u))
+            return hipErrorInvalidValue;
+        StackTable st{};
+        st.lad.s = ws.lad_s;
+        st.lad.u = ws.lad_u;
+        st.lad.d = mp.p2d;
+        st.lad.t[0] = mp.p2t;
+        return launch_apply<kApplyBuildL>(ws, mp.m, words, nw32, merge_existing, nullptr, st,
+                                          stream);
+    }
     return launch_apply<kApplyBuild>(ws, mp.m, words, nw32, merge_existing, nullptr, StackTable{},
                                      stream);
 }

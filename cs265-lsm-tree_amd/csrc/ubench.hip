@@ -177,7 +177,11 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
     const ModParams mp = make_mod_params(m);
     PartitionWorkspace ws{};
-    if (!plan_segments(m, device_cu_count(), &ws)) return -34;
+    // 20 / 21: pass 1 / pass 2 on plan_segments' segments (the round-2
+    // geometry); everything else on the product's plan_build
+    const bool seg = variant == 20 || variant == 21;
+    if (!(seg ? plan_segments(m, device_cu_count(), &ws) : plan_build(m, device_cu_count(), &ws)))
+        return -34;
     ws.tile_keys = choose_tile_keys(ws.nbins);
     ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
     ws.pos = pos;
@@ -185,8 +189,8 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     ws.run_starts = runs + ws.ntiles * (ws.nbins + 1);
     hipError_t e = hipSuccess;
     switch (variant) {
-        case 0: e = launch_part_bin(ks, mp, ws, s); break;
-        case 1: e = launch_part_apply(mp, words, ws, 0, s); break;
+        case 0: case 20: e = launch_part_bin(ks, mp, ws, s); break;
+        case 1: case 21: e = launch_part_apply(mp, words, ws, 0, s); break;
         // pass-1 shapes with the p2 remainder (MINW, NWG)
 #define UB_P2(V, TB, MAXB, MINW, NWG)                                                             \
     case V: {                                                                                    \

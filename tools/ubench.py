@@ -94,19 +94,21 @@ def part_phases(n=16_777_216, bpe=10.0, reps=50):
     torch.cuda.synchronize()
     ref = words.clone()
     names = {0: "pass 1 (product)", 1: "pass 2 (product)"}
-    for g, w in ((1, 1), (2, 1), (4, 1), (8, 1), (2, 0), (4, 0)):
-        v = 2000 + 10 * g + w
-        words.zero_()
-        if run(v) != 0:
-            continue
+    # the segment geometry (round 2) against the product's plan_build
+    words.zero_()
+    if run(20) == 0 and run(21) == 0:
         torch.cuda.synchronize()
-        ok = bool(torch.equal(ref, words))
-        print(json.dumps({"check": f"pass-2 variant {v} bitmap == product", "ok": ok}), flush=True)
-        if ok:
-            names[v] = f"pass 2 G={g} {'indep' if w else 'batch'}"
+        print(json.dumps({"check": "segment-geometry bitmap == product", "ok": bool(torch.equal(ref, words))}),
+              flush=True)
+        names[20] = "pass 1 segments"
+        names[21] = "pass 2 segments"
     _prewarm(run, 0)
     for rnd in range(2):
         for v in names:
+            if v == 21:
+                run(20)  # pass 2 over its own pass 1's output
+            elif v == 1:
+                run(0)
             ms = _events(lambda: run(v), reps)
             print(json.dumps({"op": "partition build", **geo, "phase": names[v], "round": rnd,
                               "us": round(ms * 1e3, 1)}), flush=True)
