@@ -35,8 +35,8 @@ def per_kernel_probe(d):
         base = name.split("<")[0]
         if base not in PROBE_KERNELS:
             continue
-        if base == "k_part_apply" and name.startswith("k_part_apply<0"):  # a build's pass 2
-            continue
+        if base == "k_part_apply" and name.startswith(("k_part_apply<0", "k_part_apply<4")):
+            continue  # a build's pass 2
         if base == "k_part_bin":
             targs = [a.strip() for a in name.split("<", 1)[1].split(">")[0].split(",")]
             if len(targs) > 1 and targs[1] != "true":
@@ -53,8 +53,8 @@ def per_kernel(d):
         base = name.split("<")[0]
         if base not in BUILD_KERNELS:
             continue
-        if base == "k_part_apply" and not name.startswith("k_part_apply<0"):  # probe modes
-            continue
+        if base == "k_part_apply" and not name.startswith(("k_part_apply<0", "k_part_apply<4")):
+            continue  # probe modes (builds: 0 segments, 4 plan_build's ladder)
         if base == "k_part_bin":
             targs = [a.strip() for a in name.split("<", 1)[1].split(">")[0].split(",")]
             if len(targs) > 1 and targs[1] == "true":
