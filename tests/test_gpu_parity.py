@@ -416,6 +416,34 @@ def test_probe_empty():
 
 
 # -------------------------------------------------------- full configs ----
+@pytest.mark.parametrize("m", [167_772_160, 3 * 2**26, 100_000_007], ids=["ladder", "segments", "odd_m"])
+@pytest.mark.parametrize("stride", [4, 8])
+def test_host_keys_build(torch_cuda, m, stride):
+    """A partition build from host keys (staged by the library, packed or
+    entry_t at stride 8) gives the same bitmap as one from device-resident
+    keys, also when merging into a built filter."""
+    torch = torch_cuda
+    n = (1 << 22) + 12_345
+    keys = rand_keys(n, 41)
+    if stride == 8:
+        host = np.zeros((n, 2), dtype=np.int32)
+        host[:, 0] = keys
+        host = host.reshape(-1)
+    else:
+        host = keys
+    f = bh.BloomFilter(m)
+    f.set_strategy(bh.BUILD_PARTITION)
+    f.set_batch(host, n=n, stride=stride)
+    g = bh.BloomFilter(m)
+    g.set_strategy(bh.BUILD_PARTITION)
+    g.set_batch(torch.from_numpy(keys).cuda())
+    assert (f.words() == g.words()).all()
+    more = rand_keys(n, 42)
+    f.set_batch(more)
+    g.set_batch(torch.from_numpy(more).cuda())
+    assert (f.words() == g.words()).all()
+
+
 def test_c2_full_bitmap(golden):
     from bloomhip import workloads as W
     keys, m = W.c2()

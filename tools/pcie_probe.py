@@ -52,5 +52,42 @@ def main():
     rep("h2d 67 MB || d2h 21 MB", timed(both), n_in + n_out)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(__import__("sys").argv) == 1:
     main()
+
+
+def e2e_parts():
+    """The C2 e2e build's parts: copy-then-build vs host keys staged by the
+    library, each with and without the bitmap D2H."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "cs265-lsm-tree_amd"))
+    import bloomhip as bh
+    from bloomhip import workloads as W
+    keys, m = W.c2()
+    pinned = torch.from_numpy(keys).pin_memory()
+    dk = torch.empty_like(pinned, device="cuda")
+    f = bh.BloomFilter(m)
+    hw = torch.empty(f.nwords, dtype=torch.int64).pin_memory()
+    s = torch.cuda.current_stream()
+
+    def copy_build():
+        dk.copy_(pinned, non_blocking=True)
+        f.clear(stream=s)
+        f.set_batch(dk, stream=s)
+
+    def host_build():
+        f.clear(stream=s)
+        f.set_batch(pinned, stream=s)
+
+    def dl():
+        bh.lib().bloomhip_download(f.handle, hw.data_ptr(), f.nwords, s.cuda_stream)
+    for name, fn in (("copy+build", copy_build), ("host build", host_build),
+                     ("copy+build+d2h", lambda: (copy_build(), dl())),
+                     ("host build+d2h", lambda: (host_build(), dl())), ("d2h", dl)):
+        print(json.dumps({"op": name, "ms": round(timed(fn) * 1e3, 3)}), flush=True)
+
+
+if __name__ == "__main__" and len(__import__("sys").argv) > 1:
+    e2e_parts()
