@@ -302,7 +302,9 @@ def test_stacked_probe_matches_oracle(coracle, ms):
     [5 * 2**(14 + 2 * i) for i in range(6)],      # six members, 2 KiB blocks
     [17 * 2**24, 17 * 2**20],                     # d = 17
     [5 * 2**20, 3 * 2**20, 5 * 2**18],            # two odd parts: not a ladder (segment stack)
-], ids=["c3", "d3", "uneven", "repeat", "six", "d17", "not_ladder"])
+    [3 * 2**(14 + 2 * i) for i in range(8)][::-1],  # eight members: 7 packed, byte image
+    [5 * 2**(13 + 2 * i) for i in range(7)][::-1],  # seven members
+], ids=["c3", "d3", "uneven", "repeat", "six", "d17", "not_ladder", "eight", "seven"])
 def test_ladder_stack_matches_oracle(coracle, ms):
     """Levels d << t_j probed in one ladder pass (bins = hash bits, the
     members' blocks staged per bin); every member's rows against the oracle."""
