@@ -34,6 +34,11 @@ for s in ${STEPS//,/ }; do
     ub_part) run ub_part 300 python tools/ubench.py part || exit 1 ;;
     ub_part_c5) run ub_part_c5 300 python tools/ubench.py part_c5 || exit 1 ;;
     ub_part_c4) run ub_part_c4 300 python tools/ubench.py part_c4 || exit 1 ;;
+    ub_p2ab) run ub_p2ab 300 python tools/ubench.py p2ab || exit 1 ;;
+    ub_p2ab_c5) run ub_p2ab_c5 300 python tools/ubench.py p2ab_c5 || exit 1 ;;
+    ub_p2ab_c4) run ub_p2ab_c4 300 python tools/ubench.py p2ab_c4 || exit 1 ;;
+    sq_part_c4) run sq_part_c4_a 200 timeout -s KILL 190 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d "$OUT/sq_part_c4_a" -o pmc --output-format csv -- python tools/ubench.py part_c4 || exit 1
+             run sq_part_c4_b 200 timeout -s KILL 190 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace -d "$OUT/sq_part_c4_b" -o pmc --output-format csv -- python tools/ubench.py part_c4 || exit 1 ;;
     ub_stack) run ub_stack 300 python tools/ubench.py stack || exit 1 ;;
     pcie) run pcie 120 python tools/pcie_probe.py || exit 1 ;;
     ub_ladder) run ub_ladder 300 python tools/ubench.py ladder || exit 1 ;;

@@ -144,6 +144,35 @@ def p1_ab(variants, n=16_777_216, bpe=10.0, rounds=3, reps=50):
               flush=True)
 
 
+def p2_ab(variants, n=16_777_216, bpe=10.0, rounds=3, reps=50):
+    """Interleaved A/B of pass-2 variants (ubench_part 2xxx / 3xxx) against
+    the product's pass 2 (1), all over the product's pass-1 output; each
+    variant's bitmap must equal the product's."""
+    run, words, geo = _part_setup(n, bpe)
+    assert run(0) == 0 and run(1) == 0
+    torch.cuda.synchronize()
+    ref = words.clone()
+    ok_vars = [1]
+    for v in variants:
+        words.zero_()
+        if run(v) != 0:
+            print(json.dumps({"variant": v, "skipped": "not applicable"}), flush=True)
+            continue
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(ref, words))
+        print(json.dumps({"check": f"pass-2 variant {v} bitmap == product", "ok": ok}), flush=True)
+        if ok:
+            ok_vars.append(v)
+    _prewarm(run, 1)
+    res = {v: [] for v in ok_vars}
+    for _ in range(rounds):
+        for v in res:
+            res[v].append(round(_events(lambda: run(v), reps) * 1e3, 2))
+    for v, ts in res.items():
+        print(json.dumps({"op": "pass 2 A/B", **geo, "variant": v, "us": ts, "min_us": min(ts)}),
+              flush=True)
+
+
 def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
     """The stacked C3 probe by phase (ubench_stack variants), and pass 2 with
     its result stores or 4 of its 5 member reads removed."""
@@ -321,6 +350,11 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "p1ab":
         vs = [int(v) for v in os.environ.get("UB_VARIANTS", "5001,5003").split(",")]
         return p1_ab(vs)
+    if len(sys.argv) > 1 and sys.argv[1].startswith("p2ab"):
+        vs = [int(v) for v in os.environ.get("UB_VARIANTS", "2041").split(",")]
+        size = {"p2ab": (16_777_216, 10.0, 50), "p2ab_c5": (67_108_864, 10.0, 20),
+                "p2ab_c4": (268_435_456, 12.0, 5)}[sys.argv[1]]
+        return p2_ab(vs, *size)
     if len(sys.argv) > 1 and sys.argv[1] == "part":
         return part_phases()
     if len(sys.argv) > 1 and sys.argv[1] == "part_c5":
