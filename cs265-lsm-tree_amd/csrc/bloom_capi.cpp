@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -996,8 +997,17 @@ int bloomhip_is_set(const bloomhip_filter *fc, int32_t key, int *hit_out) {
     *reinterpret_cast<volatile uint32_t *>(f->h_hit) = 2u;  // overwritten by the kernel
     hipError_t e = launch_is_set1(f->d_words, f->mp, key, f->d_hit, s);
     if (e != hipSuccess) return fail_hip(e, "k_is_set1 launch");
-    HIP_TRY(hipStreamSynchronize(s));
-    const uint32_t v = *reinterpret_cast<volatile uint32_t *>(f->h_hit);
+    // The kernel's last act is the answer's system-scope store, so once the
+    // word changes the kernel is done: spin on it (cheaper than the stream
+    // synchronisation's wake-up) for up to kIsSetSpin, then synchronise,
+    // which also reports a kernel that failed.
+    constexpr std::chrono::microseconds kIsSetSpin{1000};
+    volatile uint32_t *hv = reinterpret_cast<volatile uint32_t *>(f->h_hit);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*hv == 2u && std::chrono::steady_clock::now() - t0 < kIsSetSpin) {
+    }
+    if (*hv == 2u) HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t v = *hv;
     if (v > 1u) return fail_hip(hipErrorUnknown, "k_is_set1 result not visible");
     *hit_out = (int)v;
     return BLOOMHIP_OK;

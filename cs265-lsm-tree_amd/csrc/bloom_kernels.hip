@@ -1440,8 +1440,10 @@ __global__ void __launch_bounds__(64) k_is_set1(const uint32_t *__restrict__ wor
     if (threadIdx.x != 0) return;
     const uint64_t p1 = mod_any(raw_hash1(k), mp), p2 = mod_any(raw_hash2(k), mp),
                    p3 = mod_any(raw_hash3(k), mp);
-    *hit = (words[p1 >> 5] >> (p1 & 31)) & (words[p2 >> 5] >> (p2 & 31)) &
-           (words[p3 >> 5] >> (p3 & 31)) & 1u;
+    const uint32_t v = (words[p1 >> 5] >> (p1 & 31)) & (words[p2 >> 5] >> (p2 & 31)) &
+                       (words[p3 >> 5] >> (p3 & 31)) & 1u;
+    // system scope: the host spins on this (mapped, fine-grained) word
+    __hip_atomic_store(hit, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 inline unsigned grid_for(size_t work_items, unsigned per_block, unsigned cap) {
