@@ -148,16 +148,19 @@ def cpu_baseline_detail(keys, m):
     return out
 
 
-# The device code and its dispatch (csrc/Makefile KERNEL_SRCS)
-KERNEL_SOURCES = ("bloom_kernels.hip", "bloom_kernels.h", "bloom_math.h", "bloom_merge.hip",
-                  "bloom_merge.h", "bloom_capi.cpp")
+def kernel_sources():
+    """The device code and its dispatch: csrc/Makefile's KERNEL_SRCS, in order
+    (the list the library's compiled-in digest is taken over)."""
+    import re
+    mk = open(os.path.join(ROOT, "cs265-lsm-tree_amd", "csrc", "Makefile")).read()
+    return tuple(re.search(r"^KERNEL_SRCS\s*:?=\s*(.+)$", mk, re.M).group(1).split())
 
 
 def kernel_source_sha():
     """Digest of the kernel sources: a PMC summary counts for the bench line
     only if it was taken from exactly these kernels."""
     h = hashlib.sha256()
-    for name in KERNEL_SOURCES:
+    for name in kernel_sources():
         with open(os.path.join(ROOT, "cs265-lsm-tree_amd", "csrc", name), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]

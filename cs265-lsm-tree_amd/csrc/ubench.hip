@@ -8,7 +8,7 @@
 
 #include <algorithm>
 
-#include "bloom_kernels.hip"  // the product kernels, for ablation timing builds
+#include "bloom_device.h"  // the product kernels and launch templates, for ablation builds
 
 using namespace bloomhip;
 
@@ -205,19 +205,6 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     }
         UB_P2(5001, 512, 511, 4, 2) UB_P2(5003, 512, 511, 6, 3)
 #undef UB_P2
-        // pass 2 at G lanes per tile, W = 1 independent groups / 0 batch walk
-#define UB_P2G(G, W)                                                                              \
-    case 2000 + 10 * G + W: {                                                                    \
-        const uint64_t nw32 = ((m + 63) / 64) * 2;                                               \
-        e = ws.tile_keys == 2 * kPartTileKeys                                                   \
-                ? launch_apply_g<kApplyBuild, G, 2 * (int)kPartTileKeys, kApplyDepth, W>(        \
-                      ws, m, words, nw32, 0, nullptr, StackTable{}, s)                           \
-                : launch_apply_g<kApplyBuild, G, (int)kPartTileKeys, kApplyDepth, W>(            \
-                      ws, m, words, nw32, 0, nullptr, StackTable{}, s);                          \
-        break;                                                                                   \
-    }
-        UB_P2G(1, 1) UB_P2G(2, 1) UB_P2G(4, 1) UB_P2G(8, 1) UB_P2G(2, 0) UB_P2G(4, 0)
-#undef UB_P2G
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;
@@ -272,57 +259,12 @@ extern "C" int ubench_stack(int variant, const void *keys, size_t n, int nf, con
     }
     const ModParams mp = make_mod_params(mmax);
     const size_t nw = (n + 63) / 64;
-    const bool big = ws.tile_keys == 2 * kPartTileKeys;
     hipError_t e = hipSuccess;
     switch (variant) {
         case 0: e = launch_probe_stacked(ks, mp, st, ws, res, slots, out, nw, s); break;
         case 1: e = launch_bin<true>(ks, mp, ws, slots, s); break;
-        case 2: e = launch_apply<kApplyStack>(ws, mmax, nullptr, 0, 0, res, st, s); break;
+        case 2: e = launch_apply_stack(ws, mmax, res, st, s); break;
         case 5: e = launch_combine(ws, res, slots, n, out, nw, st, s); break;
-#define UB_SG(G)                                                                                  \
-    case 100 + G:                                                                                 \
-        e = big ? launch_apply_g<kApplyStack, G, 2 * (int)kPartTileKeys>(ws, mmax, nullptr, 0, 0, \
-                                                                        res, st, s)               \
-                : launch_apply_g<kApplyStack, G, (int)kPartTileKeys>(ws, mmax, nullptr, 0, 0,     \
-                                                                    res, st, s);                  \
-        break;
-        UB_SG(2) UB_SG(4) UB_SG(8) UB_SG(16)
-#undef UB_SG
-#define UB_SGD(G, D)                                                                              \
-    case 1000 + 10 * G + D:                                                                      \
-        e = big ? launch_apply_g<kApplyStack, G, 2 * (int)kPartTileKeys, D>(ws, mmax, nullptr, 0,  \
-                                                                           0, res, st, s)        \
-                : launch_apply_g<kApplyStack, G, (int)kPartTileKeys, D>(ws, mmax, nullptr, 0, 0,   \
-                                                                       res, st, s);              \
-        break;
-        UB_SGD(2, 1) UB_SGD(2, 4) UB_SGD(4, 1) UB_SGD(4, 4) UB_SGD(1, 2)
-#undef UB_SGD
-#define UB_SIG(G)                                                                                 \
-    case 3000 + G:                                                                               \
-        e = big ? launch_apply_g<kApplyStack, G, 2 * (int)kPartTileKeys, 1, 1>(ws, mmax, nullptr,  \
-                                                                          0, 0, res, st, s)      \
-                : launch_apply_g<kApplyStack, G, (int)kPartTileKeys, 1, 1>(ws, mmax, nullptr, 0,   \
-                                                                      0, res, st, s);            \
-        break;
-        UB_SIG(1) UB_SIG(2) UB_SIG(4) UB_SIG(8)
-#undef UB_SIG
-        // the runtime-nf kernel (the product compiles nf in): A/B of the straight-line reads
-        case 3952:
-            e = big ? launch_stack_nf<2, 2 * (int)kPartTileKeys, 1>(ws, mmax, res, st, s)
-                    : launch_stack_nf<2, (int)kPartTileKeys, 1>(ws, mmax, res, st, s);
-            break;
-        case 3954:
-            e = big ? launch_stack_nf<4, 2 * (int)kPartTileKeys, 1>(ws, mmax, res, st, s)
-                    : launch_stack_nf<4, (int)kPartTileKeys, 1>(ws, mmax, res, st, s);
-            break;
-        case 3958:
-            e = big ? launch_stack_nf<8, 2 * (int)kPartTileKeys, 0>(ws, mmax, res, st, s)
-                    : launch_stack_nf<8, (int)kPartTileKeys, 0>(ws, mmax, res, st, s);
-            break;
-        case 3900:
-            e = big ? launch_apply_g<kApplyStack, 4, 2 * (int)kPartTileKeys>(ws, mmax, nullptr, 0, 0, res, st, s)
-                    : launch_apply_g<kApplyStack, 4, (int)kPartTileKeys>(ws, mmax, nullptr, 0, 0, res, st, s);
-            break;
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;
@@ -354,29 +296,12 @@ extern "C" int ubench_ladder(int variant, int tile_keys, const void *keys, size_
     }
     const ModParams mp = make_mod_params(ms[0]);
     const size_t nw = (n + 63) / 64;
-    const bool big = ws.tile_keys == 2 * kPartTileKeys;
-    constexpr int kB = 2 * (int)kPartTileKeys, kS = (int)kPartTileKeys;
     hipError_t e = hipSuccess;
     switch (variant) {
         case 0: e = launch_probe_stacked(ks, mp, st, ws, res, slots, out, nw, s); break;
         case 1: e = launch_bin<true>(ks, mp, ws, slots, s); break;
-        case 2: e = launch_apply<kApplyLadder>(ws, ms[0], nullptr, 0, 0, res, st, s); break;
+        case 2: e = launch_apply_ladder(ws, ms[0], res, st, s); break;
         case 5: e = launch_combine(ws, res, slots, n, out, nw, st, s); break;
-#define UB_LG(G, W)                                                                        \
-    case 20 + 10 * (1 - W) + G:                                                            \
-        e = big ? launch_ladder_nf<G, kB, W>(ws, ms[0], res, st, s)                         \
-                : launch_ladder_nf<G, kS, W>(ws, ms[0], res, st, s);                        \
-        break;
-        UB_LG(2, 1) UB_LG(4, 1) UB_LG(8, 1) UB_LG(4, 0) UB_LG(8, 0) UB_LG(16, 0)
-#undef UB_LG
-        case 41:  // batch walk G = 8, one load group in flight per wave
-            e = big ? launch_ladder_nf<8, kB, 0, 1>(ws, ms[0], res, st, s)
-                    : launch_ladder_nf<8, kS, 0, 1>(ws, ms[0], res, st, s);
-            break;
-        case 44:  // batch walk G = 8, four load groups
-            e = big ? launch_ladder_nf<8, kB, 0, 4>(ws, ms[0], res, st, s)
-                    : launch_ladder_nf<8, kS, 0, 4>(ws, ms[0], res, st, s);
-            break;
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

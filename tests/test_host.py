@@ -241,28 +241,33 @@ def test_library_is_built_from_these_kernel_sources():
     # before any GPU run measures the wrong kernels
     import hashlib
     import os
+    import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
     h = hashlib.sha256()
-    for name in KERNEL_SOURCES:
+    for name in bench.kernel_sources():
         with open(os.path.join(root, "cs265-lsm-tree_amd", "csrc", name), "rb") as f:
             h.update(f.read())
     assert bh.lib().bloomhip_kernel_sha().decode() == h.hexdigest()[:16]
 
 
-# every source the device code and its dispatch are built from (the digest
-# compiled into the library; csrc/Makefile KERNEL_SRCS, bench.KERNEL_SOURCES)
-KERNEL_SOURCES = ("bloom_kernels.hip", "bloom_kernels.h", "bloom_math.h", "bloom_merge.hip",
-                  "bloom_merge.h", "bloom_capi.cpp")
-
-
-def test_digest_lists_agree():
+def test_digest_covers_every_kernel_source():
+    """csrc/Makefile's KERNEL_SRCS (the digest compiled into the library, read
+    by bench.kernel_sources) lists every device source and header of the
+    product: a kernel unit left out would change without changing the digest."""
+    import glob
     import os
-    import re
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    mk = open(os.path.join(root, "cs265-lsm-tree_amd", "csrc", "Makefile")).read()
-    srcs = re.search(r"^KERNEL_SRCS\s*:?=\s*(.+)$", mk, re.M).group(1).split()
-    assert tuple(srcs) == KERNEL_SOURCES
     sys.path.insert(0, root)
     import bench
-    assert tuple(bench.KERNEL_SOURCES) == KERNEL_SOURCES
+    csrc = os.path.join(root, "cs265-lsm-tree_amd", "csrc")
+    listed = bench.kernel_sources()
+    assert len(set(listed)) == len(listed)
+    for name in listed:
+        assert os.path.exists(os.path.join(csrc, name)), name
+    product = {os.path.basename(p) for p in glob.glob(os.path.join(csrc, "bloom_*"))
+               if p.endswith((".hip", ".h"))}
+    assert product <= set(listed), product - set(listed)
+    assert "bloom_capi.cpp" in listed
