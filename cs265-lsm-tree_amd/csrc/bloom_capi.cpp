@@ -186,9 +186,14 @@ hipError_t grow_touched(void **ptr, size_t *have, size_t need, hipStream_t s) {
 // across the build of its output run's filter cannot deadlock with trim.  The
 // workspace lock is recursive: that build takes it again (run_partition).
 // Callers hold a shared_ptr, so a workspace that bloomhip_trim drops from
-// the map stays alive until its last user is done with it.
+// the map stays alive until its last user is done with it; trim frees its
+// buffers under its lock and marks it retired, and a caller that locks a
+// retired workspace (it looked it up before trim took the map) looks up the
+// current one instead (LockedWorkspace), so no buffer is ever regrown in a
+// workspace that has left the map (it would never be freed).
 struct Workspace {
     std::recursive_mutex mu;  // held while work using the buffers is enqueued
+    bool retired = false;     // dropped from the map by bloomhip_trim (mu held)
     uint64_t *pos = nullptr;  // tile-sorted packed entries
     size_t pos_bytes = 0;
     uint32_t *runs = nullptr;  // run starts: tile-major rows, then segment-major
@@ -216,6 +221,24 @@ std::shared_ptr<Workspace> workspace_for(int device, hipStream_t s) {
     if (!w) w = std::make_shared<Workspace>();
     return w;
 }
+
+// The (device, stream) workspace, locked and live: a workspace that
+// bloomhip_trim retired between the lookup and the lock is let go and the
+// lookup repeated (trim has replaced the map by then, so this terminates).
+struct LockedWorkspace {
+    std::shared_ptr<Workspace> w;
+    std::unique_lock<std::recursive_mutex> lk;
+    LockedWorkspace(int device, hipStream_t s) {
+        for (;;) {
+            w = workspace_for(device, s);
+            lk = std::unique_lock<std::recursive_mutex>(w->mu);
+            if (!w->retired) return;
+            lk.unlock();
+        }
+    }
+    Workspace *operator->() const { return w.get(); }
+    Workspace *get() const { return w.get(); }
+};
 
 // Frees a workspace's buffers (its lock held by the caller; the stream's
 // queued work that uses them is waited for first).
@@ -403,8 +426,7 @@ int materialize_clear(bloomhip_filter *f, hipStream_t s) {
 }
 
 int run_partition(bloomhip_filter *f, const KeySpan &ks, hipStream_t s) {
-    const std::shared_ptr<Workspace> w = workspace_for(f->device, s);
-    std::lock_guard<std::recursive_mutex> lk(w->mu);
+    const LockedWorkspace w(f->device, s);
     PartitionWorkspace ws{};
     int rc = partition_workspace(w.get(), f->m, ks.n, s, &ws, /*build=*/true);
     if (rc) return rc;
@@ -782,8 +804,7 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
             st.mwords[k] = (uint32_t)(filters[mem[k]]->m / 32);
             st.row[k] = mem[k];
         }
-        const std::shared_ptr<Workspace> w = workspace_for(f0->device, s);
-        std::lock_guard<std::recursive_mutex> wl(w->mu);
+        const LockedWorkspace w(f0->device, s);
         int rc = partition_buffers(w.get(), n, s, &ws);
         if (rc) return rc;
         rc = probe_buffers(w.get(), ws, s);
@@ -824,8 +845,7 @@ int probe_rows(bloomhip_filter *f0, const bloomhip_filter *const *filters, int n
             if (e != hipSuccess) return fail_hip(e, "k_probe_lds launch");
             continue;
         }
-        const std::shared_ptr<Workspace> w = workspace_for(f0->device, s);
-        std::lock_guard<std::recursive_mutex> wl(w->mu);
+        const LockedWorkspace w(f0->device, s);
         PartitionWorkspace ws{};
         rc = partition_workspace(w.get(), filters[j]->m, n, s, &ws);
         if (rc) return rc;
@@ -988,7 +1008,10 @@ int bloomhip_is_set(const bloomhip_filter *fc, int32_t key, int *hit_out) {
     DeviceGuard g(f->device);
     std::lock_guard<std::mutex> lk(f->mu);
     if (!f->h_hit) {
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&f->h_hit), 64, hipHostMallocMapped));
+        // fine-grained (coherent) and mapped: the kernel's system-scope store
+        // is visible to the host spin below without a stream synchronisation
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&f->h_hit), 64,
+                              hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&f->d_hit), f->h_hit, 0));
     }
     hipStream_t s = nullptr;
@@ -1006,7 +1029,13 @@ int bloomhip_is_set(const bloomhip_filter *fc, int32_t key, int *hit_out) {
     const auto t0 = std::chrono::steady_clock::now();
     while (*hv == 2u && std::chrono::steady_clock::now() - t0 < kIsSetSpin) {
     }
-    if (*hv == 2u) HIP_TRY(hipStreamSynchronize(s));
+    if (*hv == 2u) {
+        HIP_TRY(hipStreamSynchronize(s));
+    } else {
+        // the answer arrived: report a launch or kernel error the spin skipped
+        const hipError_t qe = hipStreamQuery(s);
+        if (qe != hipSuccess && qe != hipErrorNotReady) return fail_hip(qe, "k_is_set1");
+    }
     const uint32_t v = *hv;
     if (v > 1u) return fail_hip(hipErrorUnknown, "k_is_set1 result not visible");
     *hit_out = (int)v;
@@ -1176,6 +1205,7 @@ int bloomhip_trim(void) {
         Workspace *w = kv.second.get();
         std::lock_guard<std::recursive_mutex> wl(w->mu);
         free_workspace_buffers(kv.first.first, kv.first.second, w);
+        w->retired = true;  // a late user looks up the map's current one
     }
     return BLOOMHIP_OK;
 }
@@ -1205,8 +1235,7 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
         // then (filter first, then workspace: the global lock order).
         std::unique_lock<std::mutex> flk;
         if (f) flk = std::unique_lock<std::mutex>(f->mu);
-        const std::shared_ptr<Workspace> w = workspace_for(device, s);
-        std::lock_guard<std::recursive_mutex> wl(w->mu);
+        const LockedWorkspace w(device, s);
         // + one entry of padding per run: merge outputs start 16-B aligned
         const size_t bytes = (std::max<uint64_t>(total, 1) + (uint64_t)nruns + 2) * 8;
         for (int i = 0; i < 2; i++) HIP_TRY(grow_touched(&w->mbuf[i], &w->mbuf_bytes[i], bytes, s));

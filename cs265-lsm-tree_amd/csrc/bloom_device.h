@@ -530,12 +530,17 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     } else if constexpr (MODE == kApplyLadder) {
         // bin b's blocks of the direct members (StackTable::lad), block q at
         // LDS word q << (s - 5); the table: row e (member 0's block, the
-        // entry's bits above s) holds, one byte each, the other direct
-        // members' blocks and the packed image's tuple; the tuple map: per
-        // tuple, the first bit of each packed member's block; then the packed
-        // image, bpp bits per position and tuple.
+        // entry's bits above s) holds rs words, one 32-bit LDS byte address
+        // each: the other direct members' blocks and the packed image's
+        // tuple; the tuple map: per tuple, the first bit of each packed
+        // member's block; then the packed image, bpp bits per position and
+        // tuple.  With a computed tuple (LK = 0) there is no table, and the
+        // tuple map lives in member 0's area until member 0 is staged.
         const LadderTable &L = st.lad;
-        constexpr uint32_t K = LK;  // direct members (L.k, compiled in)
+        // direct members (L.k, compiled in); LK = 0: one, and the packed
+        // tuple computed from the entry (LadderTable::ctup: no table)
+        constexpr uint32_t K = LK == 0 ? 1 : LK;
+        constexpr bool CT = LK == 0;
         constexpr uint32_t BPP = (uint32_t)NF - K <= 4 ? 4u : 8u;
         const uint32_t bv = L.s - 7;  // log2 of 16-B vectors per block
         const uint32_t bin = (uint32_t)b;
@@ -556,16 +561,22 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             const uint32_t hj = tj - L.s - L.u;
             return (aj << hj) | ((xs >> L.u) & ((1u << hj) - 1u));
         };
-        for (uint32_t j = 0; j < K; j++) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(st.words[j]);
-            uint4 *dst = reinterpret_cast<uint4 *>(seg) + ((size_t)L.base[j] << bv);
-            for (uint32_t q = threadIdx.x; q < (L.nblk[j] << bv); q += BLOCK)
-                dst[q] = src[(first_bit(j, q >> bv) >> 7) + (q & ((1u << bv) - 1u))];
-        }
+        auto stage_direct = [&]() {
+            for (uint32_t j = 0; j < K; j++) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(st.words[j]);
+                uint4 *dst = reinterpret_cast<uint4 *>(seg) + ((size_t)L.base[j] << bv);
+                for (uint32_t q = threadIdx.x; q < (L.nblk[j] << bv); q += BLOCK)
+                    dst[q] = src[(first_bit(j, q >> bv) >> 7) + (q & ((1u << bv) - 1u))];
+            }
+        };
+        if constexpr (!CT) stage_direct();
         uint32_t *tbl = seg + L.img_words;
-        uint32_t *tmap = tbl + L.ne * L.rs;
+        // the tuple map follows the table; with a computed tuple (no table,
+        // the images fill the LDS) it sits where member 0's blocks go, which
+        // are staged after the packed image is built from it
+        uint32_t *tmap = CT ? seg : tbl + L.ne * L.rs;
         constexpr uint32_t kTupleShift = BPP == 4 ? 0u : 1u;  // tuple words = 2^(s-3+this)
-        for (uint32_t e = threadIdx.x; e < L.ne; e += BLOCK) {
+        for (uint32_t e = CT ? L.ne : threadIdx.x; e < L.ne; e += BLOCK) {
             const uint32_t amax = e >> L.hb;
             const uint32_t xs = ((e & ((1u << L.hb) - 1u)) << L.u) | bin;  // hash bits [s, t_max)
             for (uint32_t j = 1; j < (uint32_t)NF && j <= K; j++) {
@@ -579,7 +590,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             }
         }
         if constexpr (K < (uint32_t)NF) {
-            const uint32_t tk = L.t[K], ntup = L.nblk[K];
+            const uint32_t tk = L.t[K < (uint32_t)kMaxStack ? K : 0], ntup = L.nblk[K];
             for (uint32_t tp = threadIdx.x; tp < ntup; tp += BLOCK) {
                 // tuple tp = member K's block: a_K and hash bits [s, t_K)
                 uint32_t ak, xs;
@@ -643,6 +654,10 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                 }
             }
         }
+        if constexpr (CT) {
+            __syncthreads();  // the tuple map's last reads
+            stage_direct();
+        }
     } else if constexpr (MODE == kApplyProbe) {
         for (int i = threadIdx.x; i < (int)seg_words; i += BLOCK)
             seg[i] = i < nseg ? words[w0 + i] : 0u;
@@ -664,11 +679,16 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     // prefetch included (that wait made the packed table slower than two
     // u32 columns: C2 pass 2 36 -> 41 us, C4 1.22 -> 1.56 ms).
     auto dec = [](uint32_t pk) { return make_uint2(pk & 0xFFFFu, pk >> 16); };
+    // The walk visits tiles last to first (data tile rt(t) for walk step t):
+    // pass 1 wrote them first to last, so the most recently written sorted
+    // tiles -- the ones still in the Infinity Cache -- are read first (C5
+    // pass 2 205 -> 197.5 us, C2 unchanged, profiles/r04/reverse_walk/).
+    auto rt = [&](int t) -> int { return ntiles - 1 - t; };
     auto bounds = [&](int j, uint32_t (&r)[DEPTH]) {
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) {
             const int t = j * kBatchTiles + d * kTPI + tl;
-            r[d] = t < ntiles ? run_starts[(size_t)b * ntiles + t] : 0u;
+            r[d] = t < ntiles ? run_starts[(size_t)b * ntiles + rt(t)] : 0u;
         }
     };
     // Vector vi of tile t; lanes past the tile's last vector load that one
@@ -676,7 +696,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     // clamped index would make up to G-1 lanes OR the same words, and those
     // same-address LDS atomics serialise the segments at a tile's end).
     auto load = [&](int t, uint32_t vi) -> uint4 {
-        return reinterpret_cast<const uint4 *>(pos + (size_t)t * TILE_KEYS)[min(vi, kLastVec)];
+        return reinterpret_cast<const uint4 *>(pos + (size_t)rt(t) * TILE_KEYS)[min(vi, kLastVec)];
     };
     // The six entries of vector vi of tile t; run = [r.x, r.y).
     auto apply6 = [&](const uint4 &v, int t, uint32_t vi, const uint2 &r) {
@@ -721,11 +741,26 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                     // offsets OR in).  Bit extracts take the entry itself
                     // as the shift: v_bfe_u32 uses its low 5 bits.
                     const LadderTable &L = st.lad;
-                    constexpr int K = LK;  // direct members, compiled in
+                    constexpr int K = LK == 0 ? 1 : LK;  // direct members, compiled in
+                    constexpr bool CT = LK == 0;          // packed tuple computed, no table
                     const uint32_t ee = ok ? e[k] : 0u;  // reads stay in the image
                     const uint32_t a0 = (ee >> 3) & ~3u;
                     uint32_t acc = __builtin_amdgcn_ubfe(lds_word(a0), ee, 1u);
-                    if constexpr (K > 1 || K < NF) {
+                    if constexpr (CT) {
+                        // tuple = member 1's block = hi mod nblk[1] (LadderTable::ctup)
+                        const uint32_t hi = ee >> L.s;
+                        const uint32_t tup =
+                            (uint32_t)((int)hi + __mul24((int)__umulhi(hi, L.tmagic), -(int)L.nblk[1]));
+                        uint32_t pa, psh;
+                        if constexpr (NF - 1 <= 4) {  // 8 positions per word, tuples of 2^(s-1) bytes
+                            pa = ((ee >> 1) & ((1u << (L.s - 1)) - 4u)) | ((tup << (L.s - 1)) + 4 * L.pk_words);
+                            psh = ee << 2;
+                        } else {  // 4 positions per word, tuples of 2^s bytes
+                            pa = (ee & ((1u << L.s) - 4u)) | ((tup << L.s) + 4 * L.pk_words);
+                            psh = ee << 3;
+                        }
+                        acc |= __builtin_amdgcn_ubfe(lds_word(pa), psh, (uint32_t)(NF - 1)) << 1;
+                    } else if constexpr (K > 1 || K < NF) {
                         constexpr int RW = (K - 1) + (K < NF ? 1 : 0);  // row words used
                         constexpr int RS = RW <= 1 ? 1 : RW <= 2 ? 2 : RW <= 4 ? 4 : 8;  // = L.rs
                         const uint32_t row = L.img_words * 4 + (ee >> L.s) * (4 * RS);  // byte address
@@ -789,7 +824,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             }
             // six result bytes at 6*vi (2-byte aligned): whole pairs as
             // 2-byte stores, a run's edge byte by byte
-            uint8_t *p = res + (size_t)t * kTilePos + 6 * vi;
+            uint8_t *p = res + (size_t)rt(t) * kTilePos + 6 * vi;
 #pragma unroll
             for (int q = 0; q < 3; q++) {
                 const uint32_t mq = (mask >> (2 * q)) & 3u;
@@ -814,7 +849,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         constexpr int kGroupsPerWave = 64 / G;
         const int Q = kGroupsPerWave * (BLOCK / 64);
         auto bnd = [&](int tt) -> uint32_t {  // packed; 0 = empty past the end
-            return tt < ntiles ? run_starts[(size_t)b * ntiles + tt] : 0u;
+            return tt < ntiles ? run_starts[(size_t)b * ntiles + rt(tt)] : 0u;
         };
         // the current and the next tile's bounds both stay packed (a decode
         // of the next one as it becomes current would sit between its load
@@ -1185,7 +1220,10 @@ template <int G, int TK, int WALK, int N, int D = kApplyDepth>
 hipError_t launch_ladder_k(const PartitionWorkspace &ws, uint64_t m, uint8_t *res,
                            const StackTable &st, hipStream_t stream) {
     switch (st.lad.k) {
-        case 1: return launch_apply_g<kApplyLadder, G, TK, D, WALK, N, 1>(ws, m, nullptr, 0, 0, res, st, stream);
+        case 1:
+            if (st.lad.ctup)  // the packed tuple computed (LadderTable::ctup)
+                return launch_apply_g<kApplyLadder, G, TK, D, WALK, N, 0>(ws, m, nullptr, 0, 0, res, st, stream);
+            return launch_apply_g<kApplyLadder, G, TK, D, WALK, N, 1>(ws, m, nullptr, 0, 0, res, st, stream);
         case 2: return launch_apply_g<kApplyLadder, G, TK, D, WALK, N, 2>(ws, m, nullptr, 0, 0, res, st, stream);
         case 3:
             if constexpr (N >= 3)

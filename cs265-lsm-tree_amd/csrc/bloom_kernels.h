@@ -109,6 +109,7 @@ struct PartitionWorkspace {
     uint32_t lad_hb;
 };
 
+
 inline SegMap seg_map_of(const PartitionWorkspace &ws) {
     if (ws.lad_u) return SegMap{ws.lad_s, 0, (uint32_t)ws.nbins, 0, 0, ws.lad_u, ws.lad_hb};
     return SegMap{ws.sub_shift - 1, ws.magic, (uint32_t)ws.nbins, 0, 0, 0, 0};
@@ -126,6 +127,7 @@ inline uint32_t choose_tile_keys(size_t nbins) {
 inline size_t tile_keys_of(const PartitionWorkspace &ws) {
     return ws.tile_keys ? ws.tile_keys : kPartTileKeys;
 }
+
 
 // Geometry of a stacked probe (seg_bits = w): false when no w = g << s with
 // w | m_max, w <= m_min (the smallest member), nf * w bits <= kStackMaxBits
@@ -209,6 +211,14 @@ struct LadderTable {
     uint32_t base[kMaxStack];   // direct member j's first block in the image
     uint32_t pmod[kMaxStack];   // 2^(t_max - t_j) % d
     uint32_t pmodk[kMaxStack];  // 2^(t_k - t_j) % d (packed members j > k)
+    // Computed tuple (k = 1, ctup = 1): no table.  Member 1's block for an
+    // entry with high part hi = e >> s is hi mod nblk[1] (t_1 >= s + u: the
+    // ladder identity on x >> (s + u)), i.e. hi - mulhi(hi, tmagic) * nblk[1]
+    // (tmagic = ceil(2^32 / nblk[1]), checked exact for every hi < ne), so an
+    // entry costs two LDS reads (member 0's word, the packed word) and the
+    // images may fill all of the LDS.
+    uint32_t ctup;
+    uint32_t tmagic;
 };
 
 struct StackTable {
@@ -224,10 +234,13 @@ struct StackTable {
 // fills st->lad / st->ladder and the workspace's bins; false when the members
 // do not form a ladder or no (s, u) fits the LDS image, the entry's 21 bits
 // and the table.  ncu sets u (2^u >= ncu bins).
-bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWorkspace *ws);
+// allow_computed = false: only the table forms (A/B of LadderTable::ctup).
+bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWorkspace *ws,
+                 bool allow_computed = true);
 // LDS bytes of a ladder pass 2: the images, the table, and the tuple map
 // (tuple -> packed members' blocks) used while the packed image is built.
 inline size_t ladder_lds_bytes(const LadderTable &l) {
+    if (l.ctup) return (size_t)l.img_words * 4;
     return (size_t)l.img_words * 4 + (size_t)l.ne * l.rs * 4 + (l.bpp ? (size_t)l.nblk[l.k] * 32 : 0);
 }
 

@@ -676,14 +676,16 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
 }
 
 // Ladder geometry (kernels.h LadderTable).  Of the (s, k) that fit -- the
-// entry (s bits + member 0's block index) in 21 bits, byte-sized table
-// fields (block indexes of direct members 1.. and tuples < 256), images +
-// table + tuple map in 160 KiB -- the fewest LDS reads per entry (k direct
-// members, one packed word, one table row), then the smallest image, then
-// the widest blocks.  Pass 1 tiles of 8192 keys: runs of ~96 entries per bin.
+// entry (s bits + member 0's block index) in 21 bits; images + table (one
+// 32-bit LDS byte address per direct member 1.. and for the packed tuple, rs
+// words per row) + tuple map in 160 KiB, or the images alone when the tuple
+// is computed (k = 1, LadderTable::ctup) -- the fewest LDS reads per entry
+// (k direct members, one packed word, one table row unless computed), then
+// the smallest image, then the widest blocks.  Pass 1 tiles of 8192 keys: runs of ~96 entries per bin.
 constexpr uint32_t kLadderTileKeys = 2 * (uint32_t)kPartTileKeys;
 
-bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWorkspace *ws) {
+bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWorkspace *ws,
+                 bool allow_computed) {
     if (nf < 2 || nf > kMaxStack) return false;
     uint32_t d = 0, t[kMaxStack];
     for (int j = 0; j < nf; j++) {
@@ -705,8 +707,13 @@ bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWo
     size_t best_bytes = 0;
     uint32_t best_reads = ~0u;
     for (uint32_t s = 7; s <= tmin && s + u <= tmax; s++) {
-        for (uint32_t k = 1; k <= (uint32_t)nf; k++) {
+        for (uint32_t kc = 0; kc <= (uint32_t)nf; kc++) {
+            // kc = 0: one direct member with the packed tuple computed
+            // (LadderTable::ctup, no table); kc >= 1: kc direct members
+            const uint32_t k = kc == 0 ? 1 : kc;
+            const bool ct = kc == 0;
             if (k > 3 && k < (uint32_t)nf) continue;  // the compiled-in direct counts
+            if (ct && (!allow_computed || nf < 2 || t[1] < s + u)) continue;  // member 1's block = hi mod nblk[1]
             LadderTable L{};
             L.s = s;
             L.u = u;
@@ -718,7 +725,6 @@ bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWo
             uint32_t ebits = 0;
             while ((1u << ebits) < L.ne) ebits++;
             if (s + ebits > kEntryBits) continue;
-            bool ok = true;
             uint32_t nb = 0;
             for (int j = 0; j < nf; j++) {
                 L.t[j] = t[j];
@@ -739,10 +745,23 @@ bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWo
             }
             const uint32_t rw = (k - 1) + (k < (uint32_t)nf ? 1 : 0);
             L.rs = rw <= 1 ? 1 : rw <= 2 ? 2 : rw <= 4 ? 4 : 8;
-            if (!ok) continue;
+            uint32_t reads = k + (k < (uint32_t)nf) + (k > 1 || k < (uint32_t)nf);
+            if (ct) {
+                // hi mod nblk[1] as hi - mulhi(hi, M) * nblk[1], exact for
+                // every entry high part hi < ne (checked here)
+                const uint32_t nb1 = L.nblk[1];
+                const uint32_t M = (uint32_t)(((1ull << 32) + nb1 - 1) / nb1);
+                bool exact = nb1 < (1u << 23);
+                for (uint32_t hi = 0; exact && hi < L.ne; hi++)
+                    exact = (uint32_t)(((uint64_t)hi * M) >> 32) == hi / nb1;
+                if (!exact) continue;
+                L.ctup = 1;
+                L.tmagic = M;
+                L.rs = 0;
+                reads = 2;  // member 0's word and the packed word
+            }
             const size_t bytes = ladder_lds_bytes(L);
             if (bytes > kStackMaxBits / 8) continue;
-            const uint32_t reads = k + (k < (uint32_t)nf) + (k > 1 || k < (uint32_t)nf);
             if (reads < best_reads || (reads == best_reads && bytes <= best_bytes)) {
                 best = L;  // ascending s: ties keep the wider blocks
                 best_bytes = bytes;

@@ -56,8 +56,10 @@ hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, cons
         for (int j = 0; j < st.nf; j++)
             if ((uint64_t)st.mwords[j] * 32 != ((uint64_t)L.d << L.t[j]) || L.t[j] < L.s)
                 return hipErrorInvalidValue;
-        if ((L.rs != 1 && L.rs != 2 && L.rs != 4 && L.rs != 8) || L.base[0] != 0)
+        if (L.ctup ? (L.k != 1 || L.rs != 0 || L.tmagic == 0 || L.t[1] < L.s + L.u)
+                   : (L.rs != 1 && L.rs != 2 && L.rs != 4 && L.rs != 8))
             return hipErrorInvalidValue;
+        if (L.base[0] != 0) return hipErrorInvalidValue;
         hipError_t e = launch_bin<true>(ks, mp_max, ws, slots, stream);
         if (e != hipSuccess) return e;
         e = launch_apply_ladder(ws, mp_max.m, res, st, stream);

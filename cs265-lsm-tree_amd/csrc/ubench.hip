@@ -282,7 +282,11 @@ extern "C" int ubench_ladder(int variant, int tile_keys, const void *keys, size_
     const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
     PartitionWorkspace ws{};
     StackTable st{};
-    if (!plan_ladder(ms, nf, device_cu_count(), &st, &ws)) return -34;
+    // variants >= 100: the same phase (variant - 100) on the table planner
+    // (no computed tuple, LadderTable::ctup = 0), for A/B
+    const bool table = variant >= 100 && variant < 200;
+    if (table) variant -= 100;
+    if (!plan_ladder(ms, nf, device_cu_count(), &st, &ws, !table)) return -34;
     if (tile_keys) ws.tile_keys = (uint32_t)tile_keys;
     ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
     ws.pos = pos;

@@ -110,3 +110,37 @@ def test_multi_filter_probes_in_opposite_orders_with_a_compaction(coracle):
 
     _run_all([ab, ba, compactions, trims])
     assert not bad, bad
+
+
+def test_trim_returns_device_memory_to_baseline(coracle):
+    # a caller that looked a workspace up just before bloomhip_trim
+    # took the map could regrow its buffers after trim freed them, in a
+    # workspace no longer in the map (never freed again).  Trim now retires
+    # the workspaces it takes and late callers look the map up again, so
+    # after a final trim the device's free memory is back where it was.
+    import torch
+    runs = _runs(6, [300_000, 200_000, 100_000])
+    total = sum(r.shape[0] for r in runs)
+    m = bh.m_bits(total, 10.0)
+    f = bh.BloomFilter(m)
+    want = coracle.compact(runs, False)
+    bh.compact(runs, filter=f)  # the handle's own staging exists from here on
+    bh.lib().bloomhip_trim()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+
+    def compactions():
+        for _ in range(20):
+            f.clear()
+            assert np.array_equal(bh.compact(runs, filter=f), want)
+
+    def trims():
+        for _ in range(80):
+            bh.lib().bloomhip_trim()
+
+    _run_all([compactions, compactions, trims])
+    bh.lib().bloomhip_trim()
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    # one workspace of this size is ~20 MB: a leaked one shows
+    assert free1 >= free0 - (4 << 20), (free0 - free1) / 2**20

@@ -7,10 +7,6 @@ full-size configs compare with the SHA-256 fixtures the pinned oracle wrote
 negatives, idempotence, order independence, merge = union).
 """
 import hashlib
-import os
-import subprocess
-import sys
-import textwrap
 
 import numpy as np
 import pytest
@@ -359,39 +355,57 @@ def test_stacked_probe_with_cleared_and_empty_members(coracle):
     assert not got[1].any() and not got[2].any()
 
 
-def test_stacked_probe_wraparound_windows():
-    """BLOOMHIP_STACK_WRAP=1 (read once per process, so a child process):
-    segments that do not divide the smaller members, each member staged from
-    (b*w) mod m_j with wraparound, in up to 160 KiB of LDS."""
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = textwrap.dedent(f"""
-        import sys
-        sys.path[:0] = [{os.path.join(root, 'cs265-lsm-tree_amd')!r}, {os.path.join(root, 'oracle')!r}]
-        import numpy as np
-        import bloomhip as bh
-        from bloom_oracle import COracle
-        C = COracle()
-        rng = np.random.default_rng(9)
-        for ms in ([655_360 * 4**i for i in range(5)], [3 * 2**20, 2**20, 3 * 2**18, 2**18]):
-            fs, refs = [], []
-            for j, m in enumerate(ms):
-                keys = rng.integers(-2**31, 2**31, size=40_000, dtype=np.int64).astype(np.int32)
-                f = bh.BloomFilter(m)
-                f.set_probe_strategy(bh.PROBE_STACKED)
-                f.set_batch(keys)
-                fs.append(f)
-                refs.append((m, C.build(m, keys), keys))
-            probe = rng.integers(-2**31, 2**31, size=300_001, dtype=np.int64).astype(np.int32)
-            for j, (m, w, keys) in enumerate(refs):
-                probe[j * 1000:(j + 1) * 1000] = keys[:1000]
-            got = bh.test_batch(fs, probe)
-            for j, (m, w, keys) in enumerate(refs):
-                assert (got[j] == C.test(w, m, probe)).all(), (ms, j)
-        print("ok")
-    """)
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
-                       env={**os.environ, "BLOOMHIP_STACK_WRAP": "1"})
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
+def test_stacked_probe_ladder_and_segment_geometries(coracle):
+    """AUTO/STACKED groups of both stack kinds in one process: C3's levels
+    (5 << 17, 5 << 19, ...: one odd part, a ladder stack with padded runs)
+    and a mix of odd parts (3 << 20 with powers of two: no ladder, the
+    segment stack, w | every member so each member's segment is staged
+    without wrapping).  Each member's own keys are planted in the probe."""
+    rng = np.random.default_rng(9)
+    for ms in ([655_360 * 4**i for i in range(5)], [3 * 2**20, 2**20, 3 * 2**18, 2**18]):
+        fs, refs = [], []
+        for j, m in enumerate(ms):
+            keys = rng.integers(-2**31, 2**31, size=40_000, dtype=np.int64).astype(np.int32)
+            f = bh.BloomFilter(m)
+            f.set_probe_strategy(bh.PROBE_STACKED)
+            f.set_batch(keys)
+            fs.append(f)
+            refs.append((m, coracle.build(m, keys), keys))
+        probe = rng.integers(-2**31, 2**31, size=300_001, dtype=np.int64).astype(np.int32)
+        for j, (m, w, keys) in enumerate(refs):
+            probe[j * 1000:(j + 1) * 1000] = keys[:1000]
+        got = bh.test_batch(fs, probe)
+        for j, (m, w, keys) in enumerate(refs):
+            assert (got[j] == coracle.test(w, m, probe)).all(), (ms, j)
+
+
+# m = d << t with d | 255 takes the p2 remainder on the device (bloom_math.h
+# mod_p2_hi: alignbit, v_sad_u8, mulhi, mad_i32_i24); host fuzzing covers only
+# its host form.  Every odd d | 255 across t, through the atomic build, the
+# partition build (pass-1 kinds kModP2 / kModLadder0 where t allows), the
+# gather probe and the LDS probe (m/8 <= 160 KiB).
+P2_CASES = [(d, t) for d in (3, 5, 15, 17, 51, 85, 255) for t in (12, 14, 17, 20, 21, 22)
+            if (d << t) <= (1 << 28)]
+
+
+@pytest.mark.parametrize("d,t", P2_CASES)
+def test_p2_remainder_every_odd_part(coracle, d, t):
+    m = d << t
+    keys = rand_keys(120_000, seed=d * 64 + t)
+    ref = coracle.build(m, keys)
+    built = None
+    for strategy in (bh.BUILD_ATOMIC, bh.BUILD_PARTITION, bh.BUILD_LDS):
+        f = bh.BloomFilter(m)
+        if not supported(f, strategy):
+            continue
+        f.set_batch(keys)
+        assert (f.words() == ref).all(), (d, t, strategy)
+        built = f
+    probe = np.concatenate([keys[:20_000], rand_keys(60_000, seed=7 + d + t)])
+    want = coracle.test(ref, m, probe)
+    for ps in (bh.PROBE_GATHER, bh.PROBE_LDS):  # LDS falls back to gathers above 160 KiB
+        built.set_probe_strategy(ps)
+        assert (bh.test_batch([built], probe)[0] == want).all(), (d, t, ps)
 
 
 def test_stacked_probe_profile_slot():

@@ -42,6 +42,7 @@ for s in ${STEPS//,/ }; do
     ub_stack) run ub_stack 300 python tools/ubench.py stack || exit 1 ;;
     pcie) run pcie 120 python tools/pcie_probe.py || exit 1 ;;
     ub_ladder) run ub_ladder 300 python tools/ubench.py ladder || exit 1 ;;
+    ub_chunks) run ub_chunks 300 env UB_LADDER=2,201,202,203,204,206,208 python tools/ubench.py ladder || exit 1 ;;
     ub_p1ab) run ub_p1ab 300 python tools/ubench.py p1ab || exit 1 ;;
     sq_part) run sq_part_a 150 timeout -s KILL 140 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d "$OUT/sq_part_a" -o pmc --output-format csv -- python tools/ubench.py part || exit 1
              run sq_part_b 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace -d "$OUT/sq_part_b" -o pmc --output-format csv -- python tools/ubench.py part || exit 1
@@ -53,6 +54,10 @@ for s in ${STEPS//,/ }; do
     stats_c4) run stats_c4 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c4" -o run --output-format csv -- python bench.py --workload c4 --steps 5 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
     stats_c5) run stats_c5 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c5" -o run --output-format csv -- python bench.py --workload c5 --steps 20 --warmup 3 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
     probe_sweep) run probe_sweep 300 python tools/probe_sweep.py || exit 1 ;;
+    probe_ab) run probe_ab 400 python tools/probe_ab.py 3 || exit 1 ;;
+    ab_c2) run ab_c2 600 bash tools/ab.sh "$TAG/ab_c2" 3 --no-extras --steps 200 --warmup 20 || exit 1 ;;
+    ab_c5) run ab_c5 600 bash tools/ab.sh "$TAG/ab_c5" 2 --workload c5 --no-extras --steps 20 --warmup 3 || exit 1 ;;
+    stats_c3_alt) run stats_c3_alt 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3_alt" -o run --output-format csv -- python tools/probe_prof.py auto 30 alt || exit 1 ;;
     stats_c3) run stats_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3" -o run --output-format csv -- python tools/probe_prof.py auto 30 || exit 1 ;;
     pmc_c2) pmc c2 FETCH_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
             pmc c2 WRITE_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;

@@ -7,6 +7,9 @@ import sys
 
 import torch
 
+if len(sys.argv) > 3 and sys.argv[3] == "alt":  # the lib_alt build (tools/build_alt.sh)
+    os.environ["BLOOMHIP_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
+        __file__))), "cs265-lsm-tree_amd", "lib_alt", "libbloomhip.so")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
 import bloomhip as bh  # noqa: E402

@@ -271,9 +271,11 @@ def ladder_ablation(levels_sel=(0, 1, 2, 3, 4), reps=20):
     n = gets.size
     ntiles = (n + 4095) // 4096
     dk = torch.from_numpy(gets).cuda()
-    pos = torch.empty(ntiles * 4096, dtype=torch.int64, device="cuda")
+    # padded runs (kernels.h padded_tile_entries) need up to 6 more entries
+    # per bin and tile: twice the unpadded room covers them
+    pos = torch.empty(2 * ntiles * 4096, dtype=torch.int64, device="cuda")
     runs = torch.empty(2 * ntiles * 4097, dtype=torch.int32, device="cuda")
-    res = torch.empty(ntiles * 4096 * 3, dtype=torch.uint8, device="cuda")
+    res = torch.empty(2 * ntiles * 4096 * 3, dtype=torch.uint8, device="cuda")
     slots = torch.empty(ntiles * 4096 * 3, dtype=torch.int16, device="cuda")
     out = torch.empty(nf * ((n + 63) // 64), dtype=torch.int64, device="cuda")
     s = torch.cuda.current_stream()
@@ -294,17 +296,22 @@ def ladder_ablation(levels_sel=(0, 1, 2, 3, 4), reps=20):
         return LIB.ubench_stack(v, dk.data_ptr(), n, nf, msa.ctypes.data, wp, pos.data_ptr(),
                                 runs.data_ptr(), res.data_ptr(), slots.data_ptr(), out.data_ptr(),
                                 s.cuda_stream)
+    variants = [int(v) for v in os.environ.get("UB_LADDER", "2,102").split(",")]
     for tk in (8192, 4096):
-        for v in (2, 22, 24, 28, 34, 38, 46, 41, 44):
+        for v in variants:
             out.zero_()
-            ok = run(1, tk) == 0 and run(v, tk) == 0 and run(5, tk) == 0
+            if v >= 200:  # a whole (chunked) probe
+                ok = run(v, tk) == 0
+            else:
+                b0 = 100 if v >= 100 else 0  # the table planner's own pass 1 / combine
+                ok = run(b0 + 1, tk) == 0 and run(v, tk) == 0 and run(b0 + 5, tk) == 0
             torch.cuda.synchronize()
             print(json.dumps({"check": f"ladder tk={tk} pass-2 variant {v} == segment stack",
                               "ok": bool(ok and torch.equal(ref, out))}), flush=True)
     names = {0: "all three", 1: "pass 1 (+slots)", 2: "pass 2 (product)", 5: "combine",
-             22: "pass 2 G=2", 24: "pass 2 G=4", 28: "pass 2 G=8", 34: "pass 2 batch G=4",
-             38: "pass 2 batch G=8", 46: "pass 2 batch G=16", 41: "pass 2 batch G=8 d=1",
-             44: "pass 2 batch G=8 d=4"}
+             100: "all three (table planner)", 102: "pass 2 (table planner)"}
+    names.update({v: (f"all three, chunks of {v - 200} Mi keys" if v > 200 else f"pass 2 variant {v}")
+                  for v in variants if v not in names})
     _prewarm(lambda v: run(0, 8192), 0)
     for rnd in range(2):
         t = _events(lambda: stack(0), reps)
