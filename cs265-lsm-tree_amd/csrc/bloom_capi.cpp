@@ -210,6 +210,8 @@ struct Workspace {
     size_t mcount_bytes = 0;
     int32_t *mkeys = nullptr;  // compaction: the merged run's kept keys, packed
     size_t mkeys_bytes = 0;
+    void *kway = nullptr;  // one-pass compaction: samples, partition bounds, look-back state
+    size_t kway_bytes = 0;
 };
 
 std::mutex g_ws_mu;
@@ -247,12 +249,13 @@ void free_workspace_buffers(int device, hipStream_t s, Workspace *w) {
     (void)hipStreamSynchronize(s);
     for (void **p : {(void **)&w->pos, (void **)&w->runs, (void **)&w->res, (void **)&w->slots,
                      &w->mbuf[0], &w->mbuf[1], (void **)&w->msplit, (void **)&w->mcount,
-                     (void **)&w->mkeys}) {
+                     (void **)&w->mkeys, &w->kway}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
     w->pos_bytes = w->runs_bytes = w->res_bytes = w->slots_bytes = 0;
     w->mbuf_bytes[0] = w->mbuf_bytes[1] = w->msplit_bytes = w->mcount_bytes = w->mkeys_bytes = 0;
+    w->kway_bytes = 0;
 }
 
 hipEvent_t take_event(bloomhip_filter *f) {
@@ -756,9 +759,18 @@ int effective_probe_strategy(const bloomhip_filter *f, int owner_strategy) {
 // filter first: its group is every not-yet-taken filter whose m divides its
 // m (largest first, <= kMaxStack).  A group with an explicit STACKED member
 // always runs; an AUTO group runs when it beats its members' own probes.
+// route (optional): GET routing to fuse into the combine of a stack that
+// takes every filter of the call (bloomhip_route_gets); *routed says whether
+// it was.
+struct FusedRoute {
+    const RouteTable *rt;
+    int32_t *first, *page;
+    bool routed;
+};
+
 int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int nf,
                  const KeySpan &ks, size_t n, uint64_t *dout, hipStream_t s,
-                 std::vector<char> &done) {
+                 std::vector<char> &done, FusedRoute *route = nullptr) {
     std::vector<int> cand;
     for (int j = 0; j < nf; j++) {
         const int st = effective_probe_strategy(filters[j], f0->probe_strategy);
@@ -809,9 +821,16 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
         if (rc) return rc;
         rc = probe_buffers(w.get(), ws, s);
         if (rc) return rc;
+        // every filter of a routing call in this one stack: the routing runs
+        // in its combine (k_probe_combine_route), not in k_route afterwards
+        const bool fuse = route && (int)mem.size() == nf && route->rt->nruns == nf &&
+                          (size_t)route->rt->total_fences * 4 <= kRouteLdsFenceBytes;
         hipError_t e = timed(f0, SLOT_PROBE_STACK, s, [&] {
-            return launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s);
+            return fuse ? launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s,
+                                               route->rt, route->first, route->page)
+                        : launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s);
         });
+        if (fuse && e == hipSuccess) route->routed = true;
         if (e != hipSuccess) return fail_hip(e, "stacked probe launch");
         for (int j : mem) done[j] = 1;
     }
@@ -821,11 +840,12 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
 // is_set rows of every filter for keys ks into dout (nf x ceil(n/64)), on s
 // (f0->mu held, clears materialised).
 int probe_rows(bloomhip_filter *f0, const bloomhip_filter *const *filters, int nf,
-               const KeySpan &ks, size_t n, uint64_t *dout, hipStream_t s) {
+               const KeySpan &ks, size_t n, uint64_t *dout, hipStream_t s,
+               FusedRoute *route = nullptr) {
     const size_t nw = (n + 63) / 64;
     // Groups of stacked levels first: one partitioned pass each.
     std::vector<char> done((size_t)nf, 0);
-    int rc = probe_stacks(f0, filters, nf, ks, n, dout, s, done);
+    int rc = probe_stacks(f0, filters, nf, ks, n, dout, s, done, route);
     if (rc) return rc;
     // Then, one filter at a time: small filters from LDS, large ones
     // partitioned; the rest: gathers, up to kMaxProbeFilters per launch.
@@ -971,10 +991,13 @@ int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const voi
         dfirst = first_run ? reinterpret_cast<int32_t *>(f0->d_route_stage) : nullptr;
         dpage = page ? reinterpret_cast<int32_t *>(f0->d_route_stage) + n : nullptr;
     }
-    rc = probe_rows(f0, runs, nruns, ks, n, dcand, s);
+    FusedRoute fr{&t, dfirst, dpage, false};
+    rc = probe_rows(f0, runs, nruns, ks, n, dcand, s, &fr);
     if (rc) return rc;
-    hipError_t e = launch_route(ks, t, dcand, nw, dfirst, dpage, s);
-    if (e != hipSuccess) return fail_hip(e, "k_route launch");
+    if (!fr.routed) {  // the filters were probed apart: route over their rows
+        hipError_t e = launch_route(ks, t, dcand, nw, dfirst, dpage, s);
+        if (e != hipSuccess) return fail_hip(e, "k_route launch");
+    }
     if (!out_on_device) {
         if (cand_packed)
             HIP_TRY(hipMemcpyAsync(cand_packed, dcand, cand_bytes, hipMemcpyDeviceToHost, s));
@@ -1260,8 +1283,39 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
                 off += nentries[r];
             }
         }
-        // pairwise merge rounds, the left (newer) input winning ties; round
-        // outputs alternate between the two buffers, never the round's input
+        if (!list.empty() && list.size() <= (size_t)kKwayMaxRuns) {
+            // one pass: merge + newest-wins dedup + tombstones + packed keys
+            // (bloom_merge.hip k_kway_*), into the caller's buffer or mbuf[1]
+            const void *rp[kKwayMaxRuns];
+            uint64_t rn[kKwayMaxRuns];
+            const int k = (int)list.size();
+            for (int r = 0; r < k; r++) {
+                rp[r] = list[r].first;
+                rn[r] = list[r].second;
+            }
+            HIP_TRY(grow_touched(&w->kway, &w->kway_bytes, kway_workspace_bytes(rn, k), s));
+            void *dst = out_on_device ? out_entries : w->mbuf[1];
+            hipError_t e = launch_compact_kway(rp, rn, k, drop_tombstones, dst, f ? w->mkeys : nullptr,
+                                               w->kway, w->mcount, s);
+            if (e != hipSuccess) return fail_hip(e, "k-way compaction launch");
+            uint32_t cnt = 0;
+            HIP_TRY(hipMemcpyAsync(&cnt, w->mcount, 4, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            kept = cnt;
+            if (f) {
+                int rc = kept ? set_batch_run_locked(f, w->mkeys, (size_t)kept, 4, 1, s, true)
+                              : set_batch_run_locked(f, dst, 0, 8, 1, s, true);
+                if (rc) return rc;
+            }
+            if (!out_on_device && kept)
+                HIP_TRY(hipMemcpyAsync(out_entries, dst, kept * 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            *n_out = (size_t)kept;
+            return BLOOMHIP_OK;
+        }
+        // more than kKwayMaxRuns runs: pairwise merge rounds, the left (newer)
+        // input winning ties; round outputs alternate between the two
+        // buffers, never the round's input; then the dedup pass
         int dst_buf = runs_on_device ? 0 : 1;
         while (list.size() > 1) {
             std::vector<std::pair<const char *, uint64_t>> next;

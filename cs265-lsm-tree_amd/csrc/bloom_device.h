@@ -1011,6 +1011,177 @@ __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     }
 }
 
+// The page of key k in a run (src/run.cpp:97-99): upper_bound over the run's
+// n >= 1 fences (staged in LDS at fz) minus 1, for k >= fences[0] (the range
+// check passed).  One interpolation guess from the run's first fence (f0) and
+// fence spacing (scale = (n - 1) / (last - first)) places a window of
+// kRouteWindow fences; two reads check that the answer is inside it, and 4
+// branchless halving steps find it there; when the check fails, a binary
+// search over the whole run does (exact either way, only slower).
+constexpr int kRouteWindow = 15;  // fences; answers a .. a + 15: 4 halving steps
+
+__device__ __forceinline__ int route_page(const int32_t *fz, int n, int32_t k, float f0, float scale) {
+    int a = 0;
+    bool ok = true;
+    if (n > kRouteWindow) {
+        const float gf = ((float)k - f0) * scale;
+        const int g = (int)max(gf, 0.0f);
+        a = min(max(g - kRouteWindow / 2, 0), n - kRouteWindow);
+        // the answer is in [a, a + 15] iff fences[a - 1] <= k and
+        // fences[a + 15] > k (a window at either end passes that side)
+        const int32_t fl = fz[max(a - 1, 0)], fh = fz[min(a + kRouteWindow, n - 1)];
+        ok = (a == 0 || fl <= k) && (a + kRouteWindow >= n || fh > k);
+    }
+    int lo = a;
+#pragma unroll
+    for (int st = 8; st >= 1; st >>= 1) {  // fences at index >= n count as > k
+        const int idx = lo + st - 1;
+        if (idx < n && fz[min(idx, n - 1)] <= k) lo += st;
+    }
+    if (!ok) {  // the guess missed (rare): binary search the whole run
+        int l = 1, h = n;
+        while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (fz[mid] <= k) l = mid + 1;
+            else h = mid;
+        }
+        lo = l;
+    }
+    return lo - 1;
+}
+
+// Routing fused into the stacked probe's combine (§8f row 1, Run::get's test
+// src/run.cpp:93-99 over the runs LSMTree::get visits, src/lsm_tree.cpp:
+// 141-216), when every run of the call is a member of one stack: each key's
+// member bits (the combine's AND byte) are range-checked against its runs'
+// [first fence, max key] right here, the newest candidate run is the lowest
+// set bit, its page comes from the fences staged in LDS, and the candidate
+// rows leave range-checked -- the rows are not written by the combine and
+// read back by k_route.  Persistent workgroups stage the runs' fences once.
+// Member j is run rows.row[j]; the RouteTable is indexed by run.
+template <int TILE_KEYS, int BLOCK, int LAYOUT>
+__global__ void __launch_bounds__(BLOCK) k_probe_combine_route(
+    const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, KeySpan ks,
+    uint64_t *__restrict__ out, size_t nw, StackTable rows, RouteTable rt,
+    int32_t *__restrict__ first, int32_t *__restrict__ page, size_t ntiles) {
+    constexpr int kTilePos = 3 * TILE_KEYS;
+    static_assert(BLOCK * kCombineKeys == TILE_KEYS, "8 keys per thread");
+    extern __shared__ int32_t s_fences[];
+    __shared__ __attribute__((aligned(16))) uint8_t s_r[kTilePos];
+    __shared__ int32_t s_lo[kMaxStack], s_hi[kMaxStack];
+    __shared__ uint32_t s_nf[kMaxStack], s_off[kMaxStack];
+    __shared__ float s_f0[kMaxStack], s_scale[kMaxStack];
+    __shared__ int s_run_of[kMaxStack];
+    const int nf = rows.nf;
+    for (int r = threadIdx.x; r < nf; r += BLOCK) {
+        const uint32_t n = rt.nfences[r];
+        const int32_t f0 = n ? rt.meta[r][1] : 0, fl = n ? rt.meta[r][n] : 0;
+        s_hi[r] = n ? rt.meta[r][0] : INT32_MIN;  // no fences: never in range
+        s_lo[r] = n ? f0 : INT32_MAX;
+        s_nf[r] = n;
+        s_off[r] = rt.fence_off[r];
+        s_f0[r] = (float)f0;
+        s_scale[r] = (n > 1 && fl > f0) ? (float)(n - 1) / ((float)fl - (float)f0) : 0.0f;
+        s_run_of[r] = rows.row[r];
+    }
+    for (int r = 0; r < nf; r++) {
+        const uint32_t n = rt.nfences[r];
+        const int32_t *src = rt.meta[r] + 1;
+        int32_t *dst = s_fences + rt.fence_off[r];
+        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) dst[i] = src[i];
+    }
+    const int k0 = kCombineKeys * (int)threadIdx.x;  // this thread's first key in a tile
+    const bool vec_out = ((reinterpret_cast<uintptr_t>(first) | reinterpret_cast<uintptr_t>(page)) & 15) == 0;
+    for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const size_t tile0 = tile * TILE_KEYS;
+        const int tile_keys = (int)min((size_t)TILE_KEYS, ks.n - tile0);
+        const uint4 *sl = reinterpret_cast<const uint4 *>(slots + tile * 3 * TILE_KEYS + k0);
+        const uint4 va = sl[0], vb = sl[TILE_KEYS / 8], vc = sl[2 * (TILE_KEYS / 8)];
+        int32_t key[kCombineKeys];
+        if (LAYOUT == KEYS_PACKED && tile_keys == TILE_KEYS) {
+            const int4 *kv = reinterpret_cast<const int4 *>(ks.base) + (tile0 + k0) / 4;
+            const int4 x = kv[0], y = kv[1];
+            key[0] = x.x; key[1] = x.y; key[2] = x.z; key[3] = x.w;
+            key[4] = y.x; key[5] = y.y; key[6] = y.z; key[7] = y.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < kCombineKeys; i++)
+                key[i] = k0 + i < tile_keys ? load_key<LAYOUT>(ks, tile0 + k0 + i) : 0;
+        }
+        __syncthreads();  // the previous tile's result bytes are no longer read
+        const uint4 *src = reinterpret_cast<const uint4 *>(res + tile * (size_t)kTilePos);
+        for (int q = threadIdx.x; q < kTilePos / 16; q += BLOCK) reinterpret_cast<uint4 *>(s_r)[q] = src[q];
+        __syncthreads();
+        const uint32_t a[4] = {va.x, va.y, va.z, va.w}, b[4] = {vb.x, vb.y, vb.z, vb.w},
+                       c[4] = {vc.x, vc.y, vc.z, vc.w};
+        uint32_t cand[kCombineKeys];  // bit r: run r is a candidate (filter and range)
+        int32_t fr[kCombineKeys], pg[kCombineKeys];
+#pragma unroll
+        for (int i = 0; i < kCombineKeys; i++) {
+            const int sh = 16 * (i & 1);
+            const uint32_t sa = (a[i / 2] >> sh) & 0xFFFFu, sb = (b[i / 2] >> sh) & 0xFFFFu,
+                           sc = (c[i / 2] >> sh) & 0xFFFFu;
+            const uint32_t hit = k0 + i < tile_keys ? (uint32_t)(s_r[min(sa, (uint32_t)kTilePos - 1)] &
+                                                                 s_r[min(sb, (uint32_t)kTilePos - 1)] &
+                                                                 s_r[min(sc, (uint32_t)kTilePos - 1)])
+                                                    : 0u;
+            uint32_t m = 0;
+#pragma unroll
+            for (int j = 0; j < kMaxStack; j++) {
+                if (j < nf) {
+                    const int r = s_run_of[j];
+                    const bool in = key[i] >= s_lo[r] && key[i] <= s_hi[r];
+                    m |= (((hit >> j) & 1u) & (uint32_t)in) << r;
+                }
+            }
+            cand[i] = m;
+            fr[i] = m ? __builtin_ctz(m) : -1;  // runs newest first: the lowest bit
+            pg[i] = -1;
+            if (fr[i] >= 0) {
+                const int r = fr[i];
+                pg[i] = route_page(s_fences + s_off[r], (int)s_nf[r], key[i], s_f0[r], s_scale[r]);
+            }
+        }
+        // first / page of the live keys
+        if (vec_out && tile_keys == TILE_KEYS) {
+            int4 *f4 = reinterpret_cast<int4 *>(first + tile0 + k0);
+            int4 *p4 = reinterpret_cast<int4 *>(page + tile0 + k0);
+            if (first) {
+                f4[0] = make_int4(fr[0], fr[1], fr[2], fr[3]);
+                f4[1] = make_int4(fr[4], fr[5], fr[6], fr[7]);
+            }
+            if (page) {
+                p4[0] = make_int4(pg[0], pg[1], pg[2], pg[3]);
+                p4[1] = make_int4(pg[4], pg[5], pg[6], pg[7]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kCombineKeys; i++) {
+                if (k0 + i < tile_keys) {
+                    if (first) first[tile0 + k0 + i] = fr[i];
+                    if (page) page[tile0 + k0 + i] = pg[i];
+                }
+            }
+        }
+        // candidate rows: bytes of the tile's rows that hold keys (whole
+        // 64-key words), run r's byte = bit r of the 8 keys' masks
+        if (k0 < ((tile_keys + 63) & ~63)) {
+            const uint32_t lo = cand[0] | (cand[1] << 8) | (cand[2] << 16) | (cand[3] << 24);
+            const uint32_t hi = cand[4] | (cand[5] << 8) | (cand[6] << 16) | (cand[7] << 24);
+            const size_t byte0 = tile0 / 8 + threadIdx.x;
+#pragma unroll
+            for (int r = 0; r < kMaxStack; r++) {
+                if (r < nf) {
+                    const uint32_t bl = ((lo >> r) & 0x01010101u) * 0x01020408u;
+                    const uint32_t bh = ((hi >> r) & 0x01010101u) * 0x01020408u;
+                    const uint32_t byte = (bl >> 24) | ((bh >> 20) & 0xF0u);
+                    reinterpret_cast<uint8_t *>(out + (size_t)r * nw)[byte0] = (uint8_t)byte;
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 
 // Exported by the kernel translation units (one instantiation family each).

@@ -282,9 +282,15 @@ hipError_t launch_route(const KeySpan &keys, const RouteTable &t, uint64_t *cand
 // Stacked probe of st.nf members (see StackTable) whose largest has
 // ModParams mp_max; ws from plan_stack, res/slots as for the partitioned
 // probe.  Row st.row[j] of out (nw words per row) gets member j's results.
+// rt (GET routing fused into the combine, k_probe_combine_route): every run
+// of the routing call is a member (rt->nruns == st.nf, st.row a permutation)
+// and their fences fit kRouteLdsFenceBytes; out then gets the range-checked
+// candidate rows and first / page (either may be null) what k_route writes.
 hipError_t launch_probe_stacked(const KeySpan &keys, const ModParams &mp_max, const StackTable &st,
                                 const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
-                                uint64_t *out, size_t nw, hipStream_t stream);
+                                uint64_t *out, size_t nw, hipStream_t stream,
+                                const RouteTable *rt = nullptr, int32_t *first = nullptr,
+                                int32_t *page = nullptr);
 hipError_t launch_probe_partitioned(const KeySpan &keys, const ModParams &mp, const uint32_t *words,
                                     const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
                                     uint64_t *out, hipStream_t stream);

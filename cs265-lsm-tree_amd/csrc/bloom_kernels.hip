@@ -324,7 +324,6 @@ __device__ __forceinline__ int32_t select_by_mask(uint64_t mask, int32_t r, int3
 // answer lies in it, and a branchless 4-step search finds it there.  When
 // the check fails, a binary search over the whole run does (exact either
 // way, only slower).
-constexpr int kRouteWindow = 15;  // fences; answers a .. a + 15: 4 halving steps
 
 template <int LAYOUT, bool LDS_FENCES, int NR>
 __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
@@ -410,34 +409,8 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
             // answer is in [1, n].
             const int n = (int)s_nf[fr];
             int lo;
-            bool ok = true;
             if constexpr (LDS_FENCES) {
-                const int32_t *fz = s_fences + s_off[fr];
-                int a = 0;
-                if (n > kRouteWindow) {
-                    const float gf = ((float)k - (float)s_lo[fr]) * s_scale[fr];
-                    const int g = (int)max(gf, 0.0f);
-                    a = min(max(g - kRouteWindow / 2, 0), n - kRouteWindow);
-                    // the answer is in [a, a + 15] iff fences[a - 1] <= k and
-                    // fences[a + 15] > k (a window at either end passes that side)
-                    const int32_t fl = fz[max(a - 1, 0)], fh = fz[min(a + kRouteWindow, n - 1)];
-                    ok = (a == 0 || fl <= k) && (a + kRouteWindow >= n || fh > k);
-                }
-                lo = a;
-#pragma unroll
-                for (int st = 8; st >= 1; st >>= 1) {  // fences at index >= n count as > k
-                    const int idx = lo + st - 1;
-                    if (idx < n && fz[min(idx, n - 1)] <= k) lo += st;
-                }
-                if (!ok) {  // the guess missed (rare): binary search the whole run
-                    int l = 1, h = n;
-                    while (l < h) {
-                        const int mid = (l + h) >> 1;
-                        if (fz[mid] <= k) l = mid + 1;
-                        else h = mid;
-                    }
-                    lo = l;
-                }
+                lo = route_page(s_fences + s_off[fr], n, k, (float)s_lo[fr], s_scale[fr]) + 1;
             } else {
                 // fences beyond the LDS budget: binary search in global memory
                 const int32_t *fz = t.meta[0];
@@ -451,7 +424,6 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
                 }
                 lo = l;
             }
-            (void)ok;
             pg = lo - 1;
         }
         if (valid) {

@@ -33,4 +33,16 @@ hipError_t launch_dedup(const void *in, uint64_t n, int drop_tombstones, void *o
                         uint32_t *counts_ws, hipStream_t stream, int32_t *keys_out = nullptr);
 uint64_t compact_count_words(uint64_t n);
 
+// One-pass k-way compaction (bloom_merge.hip k_kway_*): the runs (newest
+// first, each key-sorted, non-empty, 8-B aligned; k <= kKwayMaxRuns) merged
+// in (key, run, index) order, the first entry of every key kept (tombstones
+// dropped on request) and written packed to out (+ the kept keys to keys_out
+// when non-null); the kept count lands in *count_out (device u32).  ws:
+// kway_workspace_bytes(n, k), 16-B aligned.
+constexpr int kKwayMaxRuns = 8;
+uint64_t kway_workspace_bytes(const uint64_t *n, int k);
+hipError_t launch_compact_kway(const void *const *runs, const uint64_t *n, int k, int drop,
+                               void *out, int32_t *keys_out, void *ws, uint32_t *count_out,
+                               hipStream_t stream, int abl = 0);
+
 }  // namespace bloomhip

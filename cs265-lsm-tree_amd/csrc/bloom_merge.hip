@@ -267,6 +267,345 @@ __global__ void __launch_bounds__(kCompactBlock) k_compact_write(
     }
 }
 
+// ---------------------------------------------------------------------------
+// One-pass k-way compaction (k <= kKwayMaxRuns): merge, newest-wins dedup,
+// tombstone drop and the packed kept keys in ONE pass over the entries.
+//
+// Total order of all entries: (key, run, index) -- run 0 is the newest, so
+// among equal keys the newest run's first entry comes first, exactly the
+// entry MergeContext releases (src/merge.cpp:17-35); an entry is kept when its
+// key differs from its predecessor's in this order (and it is not a dropped
+// tombstone).
+//
+// Partitions: every kKwayS-th entry of every run is a sample; the samples'
+// ranks in the total order (k_kway_split: binary searches over the other
+// runs' samples) pick every kKwayQ-th sample as a partition start, and the
+// start's position in each run is found by a binary search between two of
+// that run's samples.  A partition holds exactly kKwayQ samples, so at most
+// (kKwayQ + k) * kKwayS entries: it fits one workgroup's LDS whatever the key
+// distribution or duplicates.  k_kway_merge merges a partition's k shares in
+// LDS (log2 k rounds of stable merge-path merges, the newer list on the
+// left), flags the kept entries, and places them with a decoupled look-back
+// over the partitions' kept counts (partitions taken in ticket order, so
+// every partition waits only on ones already running).
+// ---------------------------------------------------------------------------
+constexpr int kKwayS = 256;                                    // sample stride
+constexpr int kKwayQ = 8;                                      // samples per partition
+constexpr int kKwayCap = (kKwayQ + kKwayMaxRuns) * kKwayS;     // entries per partition, at most
+constexpr int kKwayBlock = 512;
+constexpr int kKwayIpt = kKwayCap / kKwayBlock;                // outputs per lane per round
+static_assert(kKwayIpt * kKwayBlock == kKwayCap, "whole outputs per lane");
+
+struct KwayRuns {
+    const Entry *run[kKwayMaxRuns];
+    uint64_t n[kKwayMaxRuns];
+    uint64_t soff[kKwayMaxRuns + 1];  // run r's samples at skeys[soff[r] .. soff[r + 1])
+    int k;
+};
+
+__global__ void __launch_bounds__(256) k_kway_samples(KwayRuns R, int32_t *__restrict__ skeys) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= R.soff[R.k]) return;
+    int r = 0;
+    while (r + 1 < R.k && R.soff[r + 1] <= g) r++;
+    skeys[g] = R.run[r][(g - R.soff[r]) * kKwayS].key;
+}
+
+// Entries of run rr before (x, r) in the total order: key < x, or key == x
+// and rr < r (a newer run's equal keys come first).
+__device__ __forceinline__ bool kway_before(int32_t key, int32_t x, int rr, int r) {
+    return key < x || (key == x && rr < r);
+}
+
+// Thread per sample: its rank; a rank that is a multiple of kKwayQ starts a
+// partition, whose bounds in every run this thread writes.
+__global__ void __launch_bounds__(256) k_kway_split(KwayRuns R, const int32_t *__restrict__ skeys,
+                                                   uint32_t *__restrict__ bounds, uint32_t nparts) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const int k = R.k;
+    if (g == 0) {
+        for (int rr = 0; rr < k; rr++) {
+            bounds[rr] = 0;
+            bounds[(size_t)nparts * kKwayMaxRuns + rr] = (uint32_t)R.n[rr];
+        }
+    }
+    if (g >= R.soff[k]) return;
+    int r = 0;
+    while (r + 1 < k && R.soff[r + 1] <= g) r++;
+    const uint64_t j = g - R.soff[r];
+    const int32_t x = skeys[g];
+    // samples of every other run before (x, r): k - 1 lower bounds, their
+    // loads interleaved (one dependent step for all runs at a time)
+    uint32_t lo[kKwayMaxRuns], hi[kKwayMaxRuns];
+    uint32_t maxlen = 0;
+#pragma unroll
+    for (int rr = 0; rr < kKwayMaxRuns; rr++) {
+        lo[rr] = 0;
+        hi[rr] = rr < k && rr != r ? (uint32_t)(R.soff[rr + 1] - R.soff[rr]) : 0u;
+        maxlen = max(maxlen, hi[rr]);
+    }
+    for (uint32_t span = maxlen; span > 0; span >>= 1) {
+#pragma unroll
+        for (int rr = 0; rr < kKwayMaxRuns; rr++) {
+            if (lo[rr] < hi[rr]) {
+                const uint32_t mid = (lo[rr] + hi[rr]) >> 1;
+                if (kway_before(skeys[R.soff[rr] + mid], x, rr, r)) lo[rr] = mid + 1;
+                else hi[rr] = mid;
+            }
+        }
+    }
+    uint64_t rank = j;
+#pragma unroll
+    for (int rr = 0; rr < kKwayMaxRuns; rr++)
+        if (rr < k && rr != r) rank += lo[rr];
+    if (rank == 0 || rank % kKwayQ != 0) return;
+    const uint64_t p = rank / kKwayQ;
+    // the partition start's position in run rr: c samples of rr come before
+    // it, so it lies in ((c - 1) * S, c * S]; a lower bound in that window
+    uint32_t a[kKwayMaxRuns], b[kKwayMaxRuns];
+    uint32_t wmax = 0;
+#pragma unroll
+    for (int rr = 0; rr < kKwayMaxRuns; rr++) {
+        const uint32_t c = lo[rr];
+        a[rr] = c > 0 ? (c - 1) * kKwayS + 1 : 0u;
+        b[rr] = rr < k && rr != r ? (uint32_t)min((uint64_t)c * kKwayS, R.n[rr]) : 0u;
+        if (rr >= k || rr == r) a[rr] = b[rr];
+        wmax = max(wmax, b[rr] - a[rr]);
+    }
+    for (uint32_t span = wmax; span > 0; span >>= 1) {
+#pragma unroll
+        for (int rr = 0; rr < kKwayMaxRuns; rr++) {
+            if (a[rr] < b[rr]) {
+                const uint32_t mid = (a[rr] + b[rr]) >> 1;
+                if (kway_before(R.run[rr][mid].key, x, rr, r)) a[rr] = mid + 1;
+                else b[rr] = mid;
+            }
+        }
+    }
+#pragma unroll
+    for (int rr = 0; rr < kKwayMaxRuns; rr++)
+        if (rr < k) bounds[p * kKwayMaxRuns + rr] = rr == r ? (uint32_t)(j * kKwayS) : a[rr];
+}
+
+// Look-back status of a partition: flag in bits 62-63 (1 = its own kept
+// count, 2 = the inclusive prefix of kept counts), value below.
+constexpr uint64_t kKwayAgg = 1ull << 62, kKwayIncl = 2ull << 62, kKwayVal = (1ull << 62) - 1;
+
+// One workgroup per partition (taken in ticket order).  One LDS buffer: each
+// merge round's outputs are computed into registers (kKwayIpt entries per
+// lane), then written back over the round's input after a barrier, so a
+// workgroup takes 32 KiB and four fit a CU (two buffers halved that: the
+// kernel is latency-bound, 8192 partitions at fan-in 4 x 4M).
+template <int ABL>
+__global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
+    KwayRuns R, const uint32_t *__restrict__ bounds, uint32_t nparts, int drop,
+    uint64_t *__restrict__ status, uint32_t *__restrict__ ticket, Entry *__restrict__ out,
+    int32_t *__restrict__ keys_out, uint32_t *__restrict__ count_out) {
+    __shared__ __attribute__((aligned(16))) Entry s_buf[kKwayCap];
+    __shared__ uint32_t s_off[kKwayMaxRuns + 1];
+    __shared__ uint32_t s_lo[kKwayMaxRuns];
+    __shared__ int32_t s_pk[kKwayMaxRuns];
+    __shared__ uint32_t s_w[kKwayBlock / 64];
+    __shared__ uint64_t s_im[kKwayBlock / 64], s_zm[kKwayBlock / 64];
+    __shared__ uint32_t s_p;
+    __shared__ uint64_t s_base;
+    __shared__ int32_t s_pred;
+    __shared__ int s_has_pred;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = R.k;
+    if (tid == 0) s_p = (ABL == 5 || ABL >= 7) ? blockIdx.x : atomicAdd(ticket, 1u);  // ticket order: predecessors are running
+    __syncthreads();
+    const uint32_t p = s_p;
+    // the shares and the entry just before the partition (its predecessor):
+    // lane r of the first wave reads run r's bounds and the key before its
+    // share, so the k runs cost two dependent memory round trips, not 2k
+    if (tid < 64) {
+        const int r = tid;
+        uint32_t lo = 0, c = 0;
+        int32_t key = 0;
+        bool has = false;
+        if (r < k) {
+            lo = bounds[(size_t)p * kKwayMaxRuns + r];
+            c = bounds[(size_t)(p + 1) * kKwayMaxRuns + r] - lo;
+            has = lo > 0;
+            if (has) key = R.run[r][lo - 1].key;
+        }
+        // exclusive prefix of the share sizes over lanes 0..k-1 (k <= 8)
+        uint32_t incl = c;
+#pragma unroll
+        for (int off = 1; off < kKwayMaxRuns; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off, 64);
+            if (r >= off) incl += o;
+        }
+        if (r < k) {
+            s_lo[r] = lo;
+            s_off[r] = incl - c;
+            s_pk[r] = has ? key : INT32_MIN;
+        }
+        if (r == k - 1) s_off[k] = incl;
+        const uint64_t hm = __ballot(has);
+        if (r == 0) s_has_pred = hm != 0;
+    }
+    __syncthreads();
+    if (tid == 0 && s_has_pred) {
+        // the total order's last entry before the partition: the largest key
+        int32_t pk = INT32_MIN;
+        bool any = false;
+        for (int r = 0; r < k; r++)
+            if (s_lo[r] > 0 && (!any || s_pk[r] >= pk)) {
+                pk = s_pk[r];
+                any = true;
+            }
+        s_pred = pk;
+    }
+    const int total = (int)s_off[k];
+    for (int r = 0; r < k; r++) {
+        const Entry *src = R.run[r] + s_lo[r];
+        const int o = (int)s_off[r], c = (int)s_off[r + 1] - o;
+        for (int i = tid; i < c; i += kKwayBlock) s_buf[o + i] = ABL == 3 ? Entry{i, i} : src[i];
+    }
+    __syncthreads();
+    // merge rounds: lists L_q = [ofs[q], ofs[q + 1]); pairs (0,1), (2,3), ...
+    // go out at the same offsets (adjacent lists merge in place of both).
+    // The list bounds live in LDS (s_off, updated between rounds): a private
+    // array indexed by the lane's pair went to scratch memory.
+    const uint32_t *ofs = s_off;
+    const int d0 = tid * kKwayIpt;  // this lane's outputs: [d0, d0 + kKwayIpt) of the partition
+    Entry mine[kKwayIpt];
+#pragma unroll
+    for (int i = 0; i < kKwayIpt; i++) mine[i] = d0 + i < total ? s_buf[d0 + i] : Entry{0, 0};
+    int nl = k;
+    while (ABL != 2 && nl > 1) {
+        const int np = (nl + 1) / 2;
+        // this lane's outputs of the round, into registers: one merge-path
+        // search where the lane enters a pair, then a sequential merge
+        int a0 = 0, a1 = 0, b1 = -1, ia = 0, ib = 0;
+#pragma unroll
+        for (int i = 0; i < kKwayIpt; i++) {
+            const int d = d0 + i;
+            if (d < total) {
+                if (d >= b1) {
+                    // the pair holding output d (pairs are consecutive output ranges)
+                    int q = 0;
+                    while (q + 1 < np && (int)ofs[min(2 * (q + 1), nl)] <= d) q++;
+                    a0 = (int)ofs[2 * q];
+                    a1 = (int)ofs[min(2 * q + 1, nl)];
+                    b1 = (int)ofs[min(2 * q + 2, nl)];
+                    const int na = a1 - a0, nb = b1 - a1, dd = d - a0;
+                    // A entries among the pair's first dd outputs (A wins ties)
+                    int lo = dd > nb ? dd - nb : 0, hi = dd < na ? dd : na;
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_buf[a0 + mid].key <= s_buf[a1 + dd - 1 - mid].key) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    ia = a0 + lo;       // absolute LDS indices of the next A and B entries
+                    ib = a1 + dd - lo;
+                }
+                const bool take_a = ia < a1 && (ib >= b1 || s_buf[ia].key <= s_buf[ib].key);
+                mine[i] = take_a ? s_buf[ia++] : s_buf[ib++];
+            }
+        }
+        __syncthreads();  // every lane's reads of this round's lists and bounds
+#pragma unroll
+        for (int i = 0; i < kKwayIpt; i++)
+            if (d0 + i < total) s_buf[d0 + i] = mine[i];
+        // the merged lists' bounds: list q of the next round is pair q
+        if (tid == 0)
+            for (int q = 1; q <= np; q++) s_off[q] = s_off[min(2 * q, nl)];
+        nl = np;
+        __syncthreads();
+    }
+    // kept flags of this lane's outputs, in order
+    uint32_t keep = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < kKwayIpt; i++) {
+        const int d = d0 + i;
+        if (d < total) {
+            const Entry e = mine[i];
+            const int32_t pkey = i > 0 ? mine[i - 1].key : d > 0 ? s_buf[d - 1].key : s_pred;
+            const bool first = d > 0 ? pkey != e.key : (!s_has_pred || s_pred != e.key);
+            const bool kk = first && !(drop && e.val == kTombstone);
+            keep |= (uint32_t)kk << i;
+            c += kk;
+        }
+    }
+    uint32_t ctot;
+    const uint32_t excl = block_exclusive_scan(c, s_w, &ctot);
+    // Decoupled look-back over the partitions' kept counts, the whole block
+    // reading 512 predecessors' states per step (one wave's 64 per step took
+    // 8 dependent steps to cross the 512 partitions running at once); the
+    // nearest inclusive prefix ends it.  Relaxed agent-scope atomics (only
+    // the counts travel).
+    if (ABL == 1 || ABL >= 7) {
+        if (tid == 0) s_base = (uint64_t)p * kKwayCap;
+    } else if (p == 0) {
+        if (tid == 0) {
+            __hip_atomic_store(&status[0], kKwayIncl | ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_base = 0;
+        }
+    } else {
+        if (tid == 0)
+            __hip_atomic_store(&status[p], kKwayAgg | ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t base = 0;
+        for (int64_t q0 = (int64_t)p - 1;;) {
+            const int64_t q = q0 - tid;  // thread 0 reads the nearest predecessor
+            const uint64_t v = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : kKwayIncl;  // before partition 0: an empty prefix
+            const uint64_t im = __ballot((v & kKwayIncl) != 0), zm = __ballot(v == 0);
+            if (lane == 0) {
+                s_im[wave] = im;
+                s_zm[wave] = zm;
+            }
+            __syncthreads();
+            // the nearest inclusive prefix: thread index F (kKwayBlock: none)
+            int F = kKwayBlock;
+            bool waiting = false;
+            for (int w = 0; w < kKwayBlock / 64; w++) {
+                const uint64_t iw = s_im[w], zw = s_zm[w];
+                if (iw) {
+                    const int fi = __builtin_ctzll(iw);
+                    waiting = (zw & (fi < 63 ? (2ull << fi) - 1 : ~0ull)) != 0;
+                    F = w * 64 + fi;
+                    break;
+                }
+                if (zw) {
+                    waiting = true;
+                    break;
+                }
+            }
+            __syncthreads();  // s_im / s_zm read by all before the next step writes them
+            if (waiting) {  // a predecessor has not published yet: read again
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint32_t tsum;
+            (void)block_exclusive_scan(tid <= F ? (uint32_t)(v & kKwayVal) : 0u, s_w, &tsum);
+            base += tsum;
+            if (F < kKwayBlock) break;
+            q0 -= kKwayBlock;
+        }
+        if (tid == 0) {
+            __hip_atomic_store(&status[p], kKwayIncl | (base + ctot), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            s_base = base;
+        }
+    }
+    if (tid == 0 && p + 1 == nparts && !(ABL == 1 || ABL >= 7)) *count_out = (uint32_t)(s_base + ctot);
+    __syncthreads();  // every lane's reads of s_buf above are done
+    // kept entries packed in place in LDS (they only move down), then written out coalesced
+    uint32_t w = excl;
+#pragma unroll
+    for (int i = 0; i < kKwayIpt; i++)
+        if ((keep >> i) & 1u) s_buf[w++] = mine[i];
+    __syncthreads();
+    const uint64_t base = s_base;
+    for (int i = tid; i < ((ABL == 6 || ABL == 8) ? 0 : (int)ctot); i += kKwayBlock) {
+        const Entry e = s_buf[i];
+        out[base + i] = e;
+        if (keys_out) keys_out[base + i] = e.key;
+    }
+}
+
 }  // namespace
 
 hipError_t launch_merge_round(const MergePairArgs *pairs, int np, uint64_t *split_ws,
@@ -323,6 +662,61 @@ hipError_t launch_dedup(const void *in, uint64_t n, int drop_tombstones, void *o
     if (err != hipSuccess || nblocks == 0) return err;
     k_compact_write<<<(unsigned)nblocks, kCompactBlock, 0, stream>>>(
         e, n, drop_tombstones, counts_ws, reinterpret_cast<Entry *>(out), keys_out);
+    return hipGetLastError();
+}
+
+}  // namespace bloomhip
+
+namespace bloomhip {
+
+uint64_t kway_parts(const uint64_t *n, int k) {
+    uint64_t ns = 0;
+    for (int r = 0; r < k; r++) ns += (n[r] + kKwayS - 1) / kKwayS;
+    return ns ? (ns - 1) / kKwayQ + 1 : 0;
+}
+
+uint64_t kway_workspace_bytes(const uint64_t *n, int k) {
+    uint64_t ns = 0;
+    for (int r = 0; r < k; r++) ns += (n[r] + kKwayS - 1) / kKwayS;
+    const uint64_t np = kway_parts(n, k);
+    // samples | bounds (np + 1 rows) | status (np) + ticket + count
+    return ((ns * 4 + 15) & ~15ull) + (np + 1) * kKwayMaxRuns * 4 + 16 + np * 8 + 16;
+}
+
+hipError_t launch_compact_kway(const void *const *runs, const uint64_t *n, int k, int drop,
+                               void *out, int32_t *keys_out, void *ws, uint32_t *count_out,
+                               hipStream_t stream, int abl) {
+    if (k < 1 || k > kKwayMaxRuns) return hipErrorInvalidValue;
+    KwayRuns R{};
+    R.k = k;
+    uint64_t ns = 0;
+    for (int r = 0; r < k; r++) {
+        if (n[r] == 0 || (reinterpret_cast<uintptr_t>(runs[r]) & 7)) return hipErrorInvalidValue;
+        R.run[r] = reinterpret_cast<const Entry *>(runs[r]);
+        R.n[r] = n[r];
+        R.soff[r] = ns;
+        ns += (n[r] + kKwayS - 1) / kKwayS;
+    }
+    R.soff[k] = ns;
+    const uint64_t np = kway_parts(n, k);
+    if (np == 0 || np >= (1ull << 31)) return hipErrorInvalidValue;
+    char *b = reinterpret_cast<char *>(ws);
+    int32_t *skeys = reinterpret_cast<int32_t *>(b);
+    b += (ns * 4 + 15) & ~15ull;
+    uint32_t *bounds = reinterpret_cast<uint32_t *>(b);
+    b += (np + 1) * kKwayMaxRuns * 4;
+    b = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(b) + 15) & ~(uintptr_t)15);
+    uint64_t *status = reinterpret_cast<uint64_t *>(b);
+    uint32_t *ticket = reinterpret_cast<uint32_t *>(status + np);
+    hipError_t e = hipMemsetAsync(status, 0, np * 8 + 4, stream);
+    if (e != hipSuccess) return e;
+    const unsigned gs = (unsigned)((ns + 255) / 256);
+    k_kway_samples<<<gs, 256, 0, stream>>>(R, skeys);
+    k_kway_split<<<gs, 256, 0, stream>>>(R, skeys, bounds, (uint32_t)np);
+#define KW(A) k_kway_merge<A><<<(unsigned)np, kKwayBlock, 0, stream>>>(R, bounds, (uint32_t)np, drop, status, \
+        ticket, reinterpret_cast<Entry *>(out), keys_out, count_out)
+    if (abl == 1) KW(1); else if (abl == 2) KW(2); else if (abl == 3) KW(3); else if (abl == 4) {}
+    else if (abl == 5) KW(5); else if (abl == 6) KW(6); else if (abl == 7) KW(7); else if (abl == 8) KW(8); else KW(0);
     return hipGetLastError();
 }
 

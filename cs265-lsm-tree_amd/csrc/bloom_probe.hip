@@ -39,10 +39,48 @@ hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, cons
     return launch_combine(ws, res, slots, ks.n, out, (ks.n + 63) / 64, rows, stream);
 }
 
+// The combine with GET routing fused in (k_probe_combine_route), when every
+// run of the routing call is a member of this stack and the runs' fences fit
+// in LDS; else hipErrorInvalidValue before anything is launched.
+hipError_t launch_combine_route(const PartitionWorkspace &ws, const uint8_t *res,
+                                const uint16_t *slots, const KeySpan &ks, uint64_t *out, size_t nw,
+                                const StackTable &rows, const RouteTable &rt, int32_t *first,
+                                int32_t *page, hipStream_t stream) {
+    if (rt.nruns != rows.nf || (size_t)rt.total_fences * 4 > kRouteLdsFenceBytes) return hipErrorInvalidValue;
+    unsigned seen = 0;
+    for (int j = 0; j < rows.nf; j++) {
+        if (rows.row[j] < 0 || rows.row[j] >= rows.nf) return hipErrorInvalidValue;
+        seen |= 1u << rows.row[j];
+    }
+    if (seen != (1u << rows.nf) - 1u) return hipErrorInvalidValue;
+    constexpr int kBig = 2 * (int)kPartTileKeys, kSmall = (int)kPartTileKeys;
+    const size_t lds = (size_t)rt.total_fences * 4;
+    const size_t cap = (size_t)device_cu_count() * 2;  // two 1024-thread workgroups per CU
+    const unsigned grid = (unsigned)(ws.ntiles < cap ? ws.ntiles : cap);
+#define COMBINE_ROUTE(TK, L)                                                                      \
+    k_probe_combine_route<TK, TK / kCombineKeys, L><<<grid, TK / kCombineKeys, lds, stream>>>(    \
+        res, slots, ks, out, nw, rows, rt, first, page, ws.ntiles)
+    const bool big = tile_keys_of(ws) == 2 * kPartTileKeys;
+    if (ks.layout == KEYS_PACKED) {
+        if (big) COMBINE_ROUTE(kBig, KEYS_PACKED); else COMBINE_ROUTE(kSmall, KEYS_PACKED);
+    } else {
+        if (big) COMBINE_ROUTE(kBig, KEYS_STRIDED); else COMBINE_ROUTE(kSmall, KEYS_STRIDED);
+    }
+#undef COMBINE_ROUTE
+    return hipGetLastError();
+}
+
 hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, const StackTable &st,
                                 const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
-                                uint64_t *out, size_t nw, hipStream_t stream) {
+                                uint64_t *out, size_t nw, hipStream_t stream, const RouteTable *rt,
+                                int32_t *first, int32_t *page) {
     if (ks.n == 0) return hipSuccess;
+    if (rt && (rt->nruns != st.nf || (size_t)rt->total_fences * 4 > kRouteLdsFenceBytes))
+        return hipErrorInvalidValue;
+    auto combine = [&]() {
+        return rt ? launch_combine_route(ws, res, slots, ks, out, nw, st, *rt, first, page, stream)
+                  : launch_combine(ws, res, slots, ks.n, out, nw, st, stream);
+    };
     if (st.ladder) {  // plan_ladder's geometry
         const LadderTable &L = st.lad;
         if (st.nf < 2 || st.nf > kMaxStack || !mp_max.fast || !mp_max.p2 || !ws.lad_u ||
@@ -64,7 +102,7 @@ hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, cons
         if (e != hipSuccess) return e;
         e = launch_apply_ladder(ws, mp_max.m, res, st, stream);
         if (e != hipSuccess) return e;
-        return launch_combine(ws, res, slots, ks.n, out, nw, st, stream);
+        return combine();
     }
     if (st.nf < 1 || st.nf > kMaxStack || !mp_max.fast || ws.seg_bits % 128 != 0 ||
         (uint64_t)ws.nbins * ws.seg_bits != mp_max.m)
@@ -77,7 +115,7 @@ hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, cons
     if (e != hipSuccess) return e;
     e = launch_apply_stack(ws, mp_max.m, res, st, stream);
     if (e != hipSuccess) return e;
-    return launch_combine(ws, res, slots, ks.n, out, nw, st, stream);
+    return combine();
 }
 
 }  // namespace bloomhip

@@ -9,6 +9,7 @@
 #include <algorithm>
 
 #include "bloom_device.h"  // the product kernels and launch templates, for ablation builds
+#include "bloom_merge.h"
 
 using namespace bloomhip;
 
@@ -322,4 +323,100 @@ extern "C" int ubench_ladder_geometry(int nf, const uint64_t *ms, uint64_t *out6
     out6[4] = st.lad.k;
     out6[5] = st.lad.bpp;
     return 0;
+}
+
+// Diagnosis of the one-pass k-way compaction (temporary): abl 0 product,
+// 1 no look-back (partition p writes at p * cap), 2 no merge rounds, 3 no
+// staging loads, 4 samples + split only.
+extern "C" int ubench_kway(int abl, const void *const *runs, const uint64_t *n, int k, void *out,
+                           int32_t *keys_out, void *ws, uint32_t *count, void *stream) {
+    return launch_compact_kway(runs, n, k, 1, out, keys_out, ws, count,
+                               reinterpret_cast<hipStream_t>(stream), abl) == hipSuccess ? 0 : -5;
+}
+extern "C" uint64_t ubench_kway_ws(const uint64_t *n, int k) { return kway_workspace_bytes(n, k); }
+
+// ---- rocprofv3 counter calibration (tools/ubench.py cal) --------------------
+// Kernels that request a known number of bytes in the access shapes the
+// product issues, so FETCH_SIZE / WRITE_SIZE can be read against them
+// (MI355X_MICROARCH.md calibrates FETCH_SIZE only for wide coalesced reads).
+// Reads (each requested byte once):
+//   0  coalesced 16-B vectors, a wave's 64 vectors contiguous (1 KiB)
+//   1  the first 64 B of every 128-B line, coalesced over lines
+//   2  one 16-B vector of every 128-B line
+//   3  pass 2's walk: the buffer as tiles x nseg runs of R vectors; block b
+//      reads segment b's run of every tile, 4 lanes per run (lane i the
+//      run's vectors i, i + 4, ...), each group of 4 its own tiles
+// Writes (each byte once):
+//   10 coalesced 16-B vector stores
+//   11 2-byte stores, three per lane at 6i, 6i + 2, 6i + 4 (the probe's
+//      result bytes along sorted runs)
+//   12 one 4-B store per 128-B line, column-major into a row-major table
+//      (pass 1's segment-major run-table columns)
+__global__ void __launch_bounds__(1024) ub_cal(uint4 *buf, size_t nv, int shape, int R, int nseg,
+                                               uint32_t *sink) {
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t nth = (size_t)gridDim.x * blockDim.x;
+    uint32_t acc = 0;
+    if (shape == 0) {
+        for (size_t i = tid; i < nv; i += nth) {
+            const uint4 v = buf[i];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    } else if (shape == 1) {
+        for (size_t i = tid; i < nv / 2; i += nth) {  // vector i of the half lines
+            const uint4 v = buf[(i / 4) * 8 + (i % 4)];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    } else if (shape == 2) {
+        for (size_t i = tid; i < nv / 8; i += nth) {
+            const uint4 v = buf[i * 8];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    } else if (shape == 3) {
+        const size_t ntiles = nv / ((size_t)nseg * R);
+        const int g = threadIdx.x / 4, gl = threadIdx.x % 4, ng = blockDim.x / 4;
+        for (int b = blockIdx.x; b < nseg; b += gridDim.x)
+            for (size_t t = g; t < ntiles; t += ng) {
+                const uint4 *run = buf + (t * nseg + b) * R;
+                for (int i = gl; i < R; i += 4) {
+                    const uint4 v = run[i];
+                    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+                }
+            }
+    } else if (shape == 10) {
+        for (size_t i = tid; i < nv; i += nth) buf[i] = make_uint4((uint32_t)i, 1, 2, 3);
+    } else if (shape == 11) {
+        uint16_t *b16 = reinterpret_cast<uint16_t *>(buf);
+        for (size_t i = tid; i < nv * 16 / 6; i += nth) {
+            b16[3 * i] = (uint16_t)i;
+            b16[3 * i + 1] = (uint16_t)(i >> 1);
+            b16[3 * i + 2] = (uint16_t)(i >> 2);
+        }
+    } else if (shape == 12) {
+        uint32_t *b32 = reinterpret_cast<uint32_t *>(buf);
+        const size_t rows = nv * 4 / 32, cols = 32;  // 128-B rows of 32 words
+        for (size_t i = tid; i < rows * cols; i += nth) b32[(i % rows) * cols + i / rows] = (uint32_t)i;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// Bytes each calibration shape requests from a buffer of nv vectors.
+extern "C" uint64_t ubench_cal_bytes(int shape, size_t nv, int R, int nseg) {
+    switch (shape) {
+        case 0: case 10: return (uint64_t)nv * 16;
+        case 1: return (uint64_t)nv * 8;
+        case 2: return (uint64_t)nv * 2;
+        case 3: return (uint64_t)(nv / ((size_t)nseg * R)) * nseg * R * 16;
+        case 11: return (uint64_t)(nv * 16 / 6) * 6;
+        case 12: return (uint64_t)nv * 16;
+        default: return 0;
+    }
+}
+
+extern "C" int ubench_cal(int shape, void *buf, size_t nv, int R, int nseg, void *stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    uint32_t *sink = reinterpret_cast<uint32_t *>(buf);  // never written for these inputs
+    const unsigned grid = shape == 3 ? (unsigned)nseg : (unsigned)(device_cu_count() * 2);
+    ub_cal<<<grid, 1024, 0, s>>>(reinterpret_cast<uint4 *>(buf), nv, shape, R, nseg, sink);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
 }

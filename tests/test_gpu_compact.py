@@ -112,3 +112,40 @@ def test_compact_device_runs_at_odd_entry_offsets(coracle):
     want = coracle.compact(runs, False)
     assert np.array_equal(np.asarray(got), want)
     assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()
+
+
+def _dup_runs(sizes, key_range, seed):
+    # sorted runs WITH repeated keys inside each run (the reference's runs
+    # never repeat a key, but MergeContext's order defines them: the first
+    # entry of the newest run holding a key wins)
+    rng = np.random.default_rng(seed)
+    runs = []
+    for n in sizes:
+        keys = np.sort(rng.integers(-key_range, key_range, size=n, dtype=np.int64).astype(np.int32))
+        vals = rng.integers(-2**31 + 1, 2**31, size=n, dtype=np.int64).astype(np.int32)
+        vals[rng.random(n) < 0.1] = TOMB
+        runs.append(np.ascontiguousarray(np.stack([keys, vals], axis=1)))
+    return runs
+
+
+@pytest.mark.parametrize("sizes,key_range", [([100_000] * 4, 5_000), ([70_000, 3, 40_000], 50),
+                                             ([300_000, 300_000], 1), ([20_000] * 8, 2_000_000)])
+@pytest.mark.parametrize("drop", [False, True])
+def test_compact_repeated_keys_across_partitions(coracle, sizes, key_range, drop):
+    # one-pass k-way path (<= 8 runs): partition starts fall inside long runs
+    # of equal keys, within and across runs; a single key repeated 600,000
+    # times still splits into bounded partitions ((key, run, index) order)
+    runs = _dup_runs(sizes, key_range, sum(sizes) % 101 + key_range)
+    got = bh.compact(runs, drop_tombstones=drop)
+    assert np.array_equal(got, coracle.compact(runs, drop))
+
+
+@pytest.mark.parametrize("drop", [False, True])
+def test_compact_more_runs_than_one_pass_takes(coracle, drop):
+    # 12 runs: beyond the one-pass kernel's 8, the pairwise merge tree + dedup
+    runs = make_runs([30_000] * 12, 200_000, 12)
+    f = bh.BloomFilter(bh.m_bits(360_000, 10.0))
+    got = bh.compact(runs, drop_tombstones=drop, filter=f)
+    want = coracle.compact(runs, drop)
+    assert np.array_equal(got, want)
+    assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()

@@ -189,3 +189,52 @@ def test_route_c3_full(coracle, golden):
     # filter bits are the pinned C3 probe results restricted by the range check
     probe = bh.test_batch(runs, gets)
     assert ((cand & ~probe) == 0).all()
+
+
+@pytest.mark.parametrize("layout", ["packed", "entry", "device"])
+def test_route_fused_into_stacked_combine(coracle, layout):
+    """Every run in one ladder stack (sizes 4096 * 4^i at 10 bits/key: m = 5 <<
+    (13 + 2i)), STACKED: the routing runs inside the stack's combine
+    (k_probe_combine_route) instead of k_route.  A skewed run (the page
+    guess misses), a run without metadata (never a candidate), a ragged
+    batch, packed / entry_t / device keys and outputs."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(31)
+    sizes = [4096, 16_384, 65_536, 262_144]
+    refs, runs = [], []
+    for j, n in enumerate(sizes):
+        if j == 2:  # skewed: a dense cluster plus a sparse tail
+            keys = np.sort(np.concatenate([rng.integers(0, 100_000, size=n - 900, dtype=np.int64),
+                                           rng.integers(-2**31, 2**31, size=900, dtype=np.int64)]))
+            keys = keys.astype(np.int32)
+        else:
+            keys = sorted_run(n, 77 + j)
+        m = bh.m_bits(n, 10.0)
+        f = bh.BloomFilter(m)
+        f.set_probe_strategy(bh.PROBE_STACKED)
+        if j == 1:
+            f.set_batch(keys)  # filter only: no run metadata
+        else:
+            f.set_batch_run(keys)
+        runs.append(f)
+        refs.append((keys, m))
+    orefs = oracle_runs(coracle, refs)
+    orefs[1] = (orefs[1][0], orefs[1][1], np.zeros(0, np.int32), 0)
+    gets = get_keys(refs, 300_001, 13)
+    wc, wf, wp = coracle.route(orefs, gets)
+    if layout == "packed":
+        cand, first, page = bh.route_gets(runs, gets)
+    elif layout == "entry":
+        aos = np.zeros((gets.size, 2), dtype=np.int32)
+        aos[:, 0] = gets
+        cand, first, page = bh.route_gets(runs, aos.reshape(-1), n=gets.size, stride=8)
+    else:
+        n = gets.size
+        dc = torch.zeros((len(runs), (n + 63) // 64), dtype=torch.int64, device="cuda")
+        df = torch.empty(n, dtype=torch.int32, device="cuda")
+        dp = torch.empty(n, dtype=torch.int32, device="cuda")
+        bh.route_gets(runs, torch.from_numpy(gets).cuda(), cand=dc, first=df, page=dp)
+        torch.cuda.synchronize()
+        cand, first, page = dc.cpu().numpy().view(np.uint64), df.cpu().numpy(), dp.cpu().numpy()
+    assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
+    assert not cand[1].any() and (first >= 0).sum() > 1000

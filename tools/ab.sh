@@ -22,7 +22,7 @@ p = d.get("probe_c3", {})
 c4 = d.get("c4_build", {})
 print(sys.argv[2], sys.argv[3], d["value"], d["ms_per_step"], x, "probe_c3", p.get("kernel_ms"),
       "c4", c4.get("gkeys_s"), c4.get("kernels"), "route", d.get("route_c3", {}).get("wall_ms"),
-      "c5", d.get("c5_eight_runs", {}).get("gkeys_s"))
+      "c5", d.get("c5_eight_runs", {}).get("gkeys_s"), "compact", d.get("compact_fanin4", {}).get("ms"))
 PY
   done
 done

@@ -56,7 +56,10 @@ for s in ${STEPS//,/ }; do
     probe_sweep) run probe_sweep 300 python tools/probe_sweep.py || exit 1 ;;
     probe_ab) run probe_ab 400 python tools/probe_ab.py 3 || exit 1 ;;
     ab_c2) run ab_c2 600 bash tools/ab.sh "$TAG/ab_c2" 3 --no-extras --steps 200 --warmup 20 || exit 1 ;;
+    ab_full) run ab_full 900 bash tools/ab.sh "$TAG/ab_full" 2 --no-c4 --no-c5 --steps 100 --warmup 10 || exit 1 ;;
     ab_c5) run ab_c5 600 bash tools/ab.sh "$TAG/ab_c5" 2 --workload c5 --no-extras --steps 20 --warmup 3 || exit 1 ;;
+    stats_compact) run stats_compact 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_compact" -o run --output-format csv -- python tools/compact_prof.py 40 || exit 1 ;;
+    stats_compact_alt) run stats_compact_alt 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_compact_alt" -o run --output-format csv -- python tools/compact_prof.py 40 alt || exit 1 ;;
     stats_c3_alt) run stats_c3_alt 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3_alt" -o run --output-format csv -- python tools/probe_prof.py auto 30 alt || exit 1 ;;
     stats_c3) run stats_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3" -o run --output-format csv -- python tools/probe_prof.py auto 30 || exit 1 ;;
     pmc_c2) pmc c2 FETCH_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
@@ -67,6 +70,12 @@ for s in ${STEPS//,/ }; do
             run pmc_c3_WRITE_SIZE 150 timeout -s KILL 140 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_c3_WRITE_SIZE" -o pmc --output-format csv -- python tools/probe_prof.py auto 10 || exit 1 ;;
     bench_dist2) run bench_dist2 600 env BLOOMHIP_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline || exit 1 ;;
     bench_driver) run bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
+    cal) run cal 120 python tools/ubench.py cal || exit 1
+         for c in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_32B_sum" \
+                  "TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"; do
+           n=$(echo $c | cut -d' ' -f1)
+           run "cal_$n" 150 timeout -s KILL 140 rocprofv3 --pmc $c --kernel-trace -d "$OUT/cal_$n" -o pmc --output-format csv -- python tools/ubench.py cal || exit 1
+         done ;;
     pmc_c5) pmc c5 FETCH_SIZE --workload c5 --steps 5 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
             pmc c5 WRITE_SIZE --workload c5 --steps 5 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -344,10 +344,51 @@ def mixed():
                           "sum": round((t["valu only"] + t["lds only"]) * 1e3, 1)}), flush=True)
 
 
+LIB.ubench_cal.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                           ctypes.c_int, ctypes.c_void_p]
+LIB.ubench_cal_bytes.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+LIB.ubench_cal_bytes.restype = ctypes.c_uint64
+
+CAL_SHAPES = [(0, 1, 1, "read: coalesced 16-B vectors"), (1, 1, 1, "read: first 64 B of each 128-B line"),
+              (2, 1, 1, "read: one 16-B vector per 128-B line"),
+              (3, 1, 2458, "read: pass-2 walk, runs of 1 vector, 2458 segments (C4)"),
+              (3, 2, 2458, "read: pass-2 walk, runs of 2 vectors, 2458 segments (C4)"),
+              (3, 8, 256, "read: pass-2 walk, runs of 8 vectors, 256 segments (C2)"),
+              (3, 16, 256, "read: pass-2 walk, runs of 16 vectors, 256 segments (C3)"),
+              (10, 1, 1, "write: coalesced 16-B vectors"),
+              (11, 1, 1, "write: 2-byte stores at 6i, 6i+2, 6i+4 (probe result bytes)"),
+              (12, 1, 1, "write: one 4-B store per 128-B line (run-table columns)")]
+
+
+def cal():
+    """Calibration shapes (ubench_cal) over a 512 MiB buffer (beyond the
+    Infinity Cache), three dispatches each; run under rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE, then tools/pmc_cal.py reads the counters against
+    the known bytes printed here."""
+    nv = (512 << 20) // 16
+    buf = torch.zeros(nv * 4, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    for i, (shape, R, nseg, name) in enumerate(CAL_SHAPES):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        assert LIB.ubench_cal(shape, buf.data_ptr(), nv, R, nseg, s.cuda_stream) == 0
+        a.record(s)
+        for rep in range(2):
+            assert LIB.ubench_cal(shape, buf.data_ptr(), nv, R, nseg, s.cuda_stream) == 0
+        b.record(s)
+        torch.cuda.synchronize()
+        known = int(LIB.ubench_cal_bytes(shape, nv, R, nseg))
+        us = a.elapsed_time(b) / 2 * 1e3
+        print(json.dumps({"cal": i, "shape": shape, "R": R, "nseg": nseg, "what": name,
+                          "known_bytes": known, "us": round(us, 1),
+                          "known_GBps": round(known / us / 1e3, 1)}), flush=True)
+
+
 def main():
     torch.cuda.set_device(0)
     if len(sys.argv) > 1 and sys.argv[1] == "mixed":
         return mixed()
+    if len(sys.argv) > 1 and sys.argv[1] == "cal":
+        return cal()
     if len(sys.argv) > 1 and sys.argv[1] == "ladder":
         ladder_ablation()
         return ladder_ablation((0, 1, 2, 3))
