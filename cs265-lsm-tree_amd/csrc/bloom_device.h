@@ -1136,11 +1136,51 @@ __global__ void __launch_bounds__(BLOCK) k_probe_combine_route(
             }
             cand[i] = m;
             fr[i] = m ? __builtin_ctz(m) : -1;  // runs newest first: the lowest bit
-            pg[i] = -1;
-            if (fr[i] >= 0) {
-                const int r = fr[i];
-                pg[i] = route_page(s_fences + s_off[r], (int)s_nf[r], key[i], s_f0[r], s_scale[r]);
+        }
+        // The pages of the lane's 8 keys, searched side by side (each step's
+        // 8 LDS reads independent; one key at a time was 8 chains of
+        // dependent reads): the window guess and its check, 4 halving steps,
+        // and the whole-run binary search for the rare key whose guess missed.
+        int base_[kCombineKeys], n_[kCombineKeys], lo_[kCombineKeys];
+        bool ok_[kCombineKeys];
+#pragma unroll
+        for (int i = 0; i < kCombineKeys; i++) {
+            const int r = max(fr[i], 0);
+            base_[i] = (int)s_off[r];
+            n_[i] = fr[i] >= 0 ? (int)s_nf[r] : 0;
+            int a = 0;
+            ok_[i] = true;
+            if (n_[i] > kRouteWindow) {
+                const int g = (int)max(((float)key[i] - s_f0[r]) * s_scale[r], 0.0f);
+                a = min(max(g - kRouteWindow / 2, 0), n_[i] - kRouteWindow);
+                const int32_t fl = s_fences[base_[i] + max(a - 1, 0)];
+                const int32_t fh = s_fences[base_[i] + min(a + kRouteWindow, n_[i] - 1)];
+                ok_[i] = (a == 0 || fl <= key[i]) && (a + kRouteWindow >= n_[i] || fh > key[i]);
             }
+            lo_[i] = a;
+        }
+#pragma unroll
+        for (int st = 8; st >= 1; st >>= 1) {
+#pragma unroll
+            for (int i = 0; i < kCombineKeys; i++) {
+                const int idx = lo_[i] + st - 1;
+                const int32_t f = s_fences[base_[i] + min(idx, max(n_[i] - 1, 0))];
+                if (idx < n_[i] && f <= key[i]) lo_[i] += st;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kCombineKeys; i++) {
+            if (!ok_[i]) {  // the guess missed (rare): binary search the whole run
+                const int32_t *fz = s_fences + base_[i];
+                int l = 1, h = n_[i];
+                while (l < h) {
+                    const int mid = (l + h) >> 1;
+                    if (fz[mid] <= key[i]) l = mid + 1;
+                    else h = mid;
+                }
+                lo_[i] = l;
+            }
+            pg[i] = fr[i] >= 0 ? lo_[i] - 1 : -1;
         }
         // first / page of the live keys
         if (vec_out && tile_keys == TILE_KEYS) {

@@ -404,7 +404,6 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
     __shared__ __attribute__((aligned(16))) Entry s_buf[kKwayCap];
     __shared__ uint32_t s_off[kKwayMaxRuns + 1];
     __shared__ uint32_t s_lo[kKwayMaxRuns];
-    __shared__ int32_t s_pk[kKwayMaxRuns];
     __shared__ uint32_t s_w[kKwayBlock / 64];
     __shared__ uint64_t s_im[kKwayBlock / 64], s_zm[kKwayBlock / 64];
     __shared__ uint32_t s_p;
@@ -416,18 +415,13 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
     __syncthreads();
     const uint32_t p = s_p;
     // the shares and the entry just before the partition (its predecessor):
-    // lane r of the first wave reads run r's bounds and the key before its
-    // share, so the k runs cost two dependent memory round trips, not 2k
+    // lane r of the first wave reads run r's bounds
     if (tid < 64) {
         const int r = tid;
         uint32_t lo = 0, c = 0;
-        int32_t key = 0;
-        bool has = false;
         if (r < k) {
             lo = bounds[(size_t)p * kKwayMaxRuns + r];
             c = bounds[(size_t)(p + 1) * kKwayMaxRuns + r] - lo;
-            has = lo > 0;
-            if (has) key = R.run[r][lo - 1].key;
         }
         // exclusive prefix of the share sizes over lanes 0..k-1 (k <= 8)
         uint32_t incl = c;
@@ -439,40 +433,57 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
         if (r < k) {
             s_lo[r] = lo;
             s_off[r] = incl - c;
-            s_pk[r] = has ? key : INT32_MIN;
         }
         if (r == k - 1) s_off[k] = incl;
-        const uint64_t hm = __ballot(has);
-        if (r == 0) s_has_pred = hm != 0;
     }
     __syncthreads();
-    if (tid == 0 && s_has_pred) {
-        // the total order's last entry before the partition: the largest key
-        int32_t pk = INT32_MIN;
-        bool any = false;
-        for (int r = 0; r < k; r++)
-            if (s_lo[r] > 0 && (!any || s_pk[r] >= pk)) {
-                pk = s_pk[r];
-                any = true;
-            }
-        s_pred = pk;
-    }
     const int total = (int)s_off[k];
-    for (int r = 0; r < k; r++) {
-        const Entry *src = R.run[r] + s_lo[r];
-        const int o = (int)s_off[r], c = (int)s_off[r + 1] - o;
-        for (int i = tid; i < c; i += kKwayBlock) s_buf[o + i] = ABL == 3 ? Entry{i, i} : src[i];
+    // every load of the partition in flight at once: this lane's kKwayIpt
+    // positions of the concatenated shares (strided, so each load instruction
+    // is coalesced), and (lanes 0..k-1) the key just before run r's share; a
+    // load-then-store loop per run waited for each run's loads in turn
+    const int d0 = tid * kKwayIpt;  // this lane's outputs of the merge: [d0, d0 + kKwayIpt)
+    Entry mine[kKwayIpt];
+    {
+        int r = 0;
+#pragma unroll
+        for (int i = 0; i < kKwayIpt; i++) {
+            const int d = tid + i * kKwayBlock;
+            if (d < total) {
+                while ((int)s_off[r + 1] <= d) r++;
+                mine[i] = ABL == 3 ? Entry{d, d} : R.run[r][s_lo[r] + (uint32_t)(d - (int)s_off[r])];
+            }
+        }
     }
+    int32_t pkey = INT32_MIN;
+    const bool phas = tid < k && s_lo[tid] > 0;
+    if (phas) pkey = R.run[tid][s_lo[tid] - 1].key;
+    {
+        // the total order's last entry before the partition: the largest key
+        const uint64_t hm = __ballot(phas);
+        int32_t mk = phas ? pkey : INT32_MIN;
+        if (tid < 64) {
+#pragma unroll
+            for (int off = 4; off >= 1; off >>= 1) mk = max(mk, __shfl_xor(mk, off, 64));
+            if (tid == 0) {
+                s_has_pred = hm != 0;
+                s_pred = mk;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kKwayIpt; i++)
+        if (tid + i * kKwayBlock < total) s_buf[tid + i * kKwayBlock] = mine[i];
     __syncthreads();
+    if (k == 1) {  // no merge round: this lane's outputs straight from the staged run
+#pragma unroll
+        for (int i = 0; i < kKwayIpt; i++) mine[i] = d0 + i < total ? s_buf[d0 + i] : Entry{0, 0};
+    }
     // merge rounds: lists L_q = [ofs[q], ofs[q + 1]); pairs (0,1), (2,3), ...
     // go out at the same offsets (adjacent lists merge in place of both).
     // The list bounds live in LDS (s_off, updated between rounds): a private
     // array indexed by the lane's pair went to scratch memory.
     const uint32_t *ofs = s_off;
-    const int d0 = tid * kKwayIpt;  // this lane's outputs: [d0, d0 + kKwayIpt) of the partition
-    Entry mine[kKwayIpt];
-#pragma unroll
-    for (int i = 0; i < kKwayIpt; i++) mine[i] = d0 + i < total ? s_buf[d0 + i] : Entry{0, 0};
     int nl = k;
     while (ABL != 2 && nl > 1) {
         const int np = (nl + 1) / 2;
@@ -544,8 +555,15 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
             s_base = 0;
         }
     } else {
-        if (tid == 0)
+        if (tid == 0) {
             __hip_atomic_store(&status[p], kKwayAgg | ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // wait for the nearest predecessor alone (one load per try) before
+            // reading the window: 512 loads per try while it runs would load
+            // the memory system for every other workgroup
+            while (__hip_atomic_load(&status[p - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                __builtin_amdgcn_s_sleep(2);
+        }
+        __syncthreads();
         uint64_t base = 0;
         for (int64_t q0 = (int64_t)p - 1;;) {
             const int64_t q = q0 - tid;  // thread 0 reads the nearest predecessor

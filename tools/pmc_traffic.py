@@ -1,8 +1,19 @@
 #!/usr/bin/env python3
 """HBM bytes per build from two rocprofv3 PMC passes (tools/gpu_prof.sh):
-FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE is doubled (the gfx950
-correction of MI355X_MICROARCH.md, HBM section: it tallies 128-B requests at
-64 B).  Per kernel, the median over the dispatches of its largest grid (the
+FETCH_SIZE and WRITE_SIZE are in KiB.  FETCH_SIZE is doubled and WRITE_SIZE
+taken as it is, by the calibration of every access shape the product issues
+(profiles/pmc_calibration.json, tools/ubench.py cal + tools/pmc_cal.py): on
+gfx950 every read request the L2 sends is a whole 128-B line tallied at 64 B
+(TCC_BUBBLE stays 0, FETCH_SIZE = TCC_EA0_RDREQ x 64 B), whatever part of
+the line the kernel asked for -- coalesced vectors 0.50, half lines 1.00, one
+16-B vector per line 4.00, pass 2's walk over runs of 1 / 2 / 8 / 16 vectors
+4.00 / 2.00 / 0.50 / 0.50 of the requested bytes, and the half-line and
+vector-per-line reads take as long as reading every whole line -- so 2 x
+FETCH_SIZE is the line traffic in each shape; WRITE_SIZE equals the stored
+bytes for 16-B vector stores and for 2-byte stores that fill their lines
+(WRREQ_64B), and counts 32 B per isolated 4-B store (8x: the run table's
+column stores), which is the request the memory receives.
+Per kernel, the median over the dispatches of its largest grid (the
 workload's own build; smaller grids are the tests' warm-up builds).
 
 Usage: pmc_traffic.py WORKLOAD TAG  -> profiles/pmc_WORKLOAD.json
