@@ -1060,7 +1060,7 @@ __device__ __forceinline__ int route_page(const int32_t *fz, int n, int32_t k, f
 // read back by k_route.  Persistent workgroups stage the runs' fences once.
 // Member j is run rows.row[j]; the RouteTable is indexed by run.
 template <int TILE_KEYS, int BLOCK, int LAYOUT>
-__global__ void __launch_bounds__(BLOCK) k_probe_combine_route(
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) k_probe_combine_route(
     const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, KeySpan ks,
     uint64_t *__restrict__ out, size_t nw, StackTable rows, RouteTable rt,
     int32_t *__restrict__ first, int32_t *__restrict__ page, size_t ntiles) {
@@ -1114,7 +1114,7 @@ __global__ void __launch_bounds__(BLOCK) k_probe_combine_route(
         __syncthreads();
         const uint32_t a[4] = {va.x, va.y, va.z, va.w}, b[4] = {vb.x, vb.y, vb.z, vb.w},
                        c[4] = {vc.x, vc.y, vc.z, vc.w};
-        uint32_t cand[kCombineKeys];  // bit r: run r is a candidate (filter and range)
+        uint32_t cand_lo = 0, cand_hi = 0;  // byte i: key i's candidate runs (bit r: filter and range)
         int32_t fr[kCombineKeys], pg[kCombineKeys];
 #pragma unroll
         for (int i = 0; i < kCombineKeys; i++) {
@@ -1134,53 +1134,61 @@ __global__ void __launch_bounds__(BLOCK) k_probe_combine_route(
                     m |= (((hit >> j) & 1u) & (uint32_t)in) << r;
                 }
             }
-            cand[i] = m;
+            if (i < 4) cand_lo |= m << (8 * i);
+            else cand_hi |= m << (8 * (i - 4));
             fr[i] = m ? __builtin_ctz(m) : -1;  // runs newest first: the lowest bit
         }
-        // The pages of the lane's 8 keys, searched side by side (each step's
-        // 8 LDS reads independent; one key at a time was 8 chains of
-        // dependent reads): the window guess and its check, 4 halving steps,
+        // The pages of the lane's keys, two searched side by side (their LDS
+        // reads independent; all 8 at once took 89 VGPRs, which left one
+        // 1024-lane workgroup per CU, and 4 spilled under the 64-VGPR cap
+        // that fits two): the window guess and its check, 4 halving steps,
         // and the whole-run binary search for the rare key whose guess missed.
-        int base_[kCombineKeys], n_[kCombineKeys], lo_[kCombineKeys];
-        bool ok_[kCombineKeys];
+        constexpr int kSide = 2;
 #pragma unroll
-        for (int i = 0; i < kCombineKeys; i++) {
-            const int r = max(fr[i], 0);
-            base_[i] = (int)s_off[r];
-            n_[i] = fr[i] >= 0 ? (int)s_nf[r] : 0;
-            int a = 0;
-            ok_[i] = true;
-            if (n_[i] > kRouteWindow) {
-                const int g = (int)max(((float)key[i] - s_f0[r]) * s_scale[r], 0.0f);
-                a = min(max(g - kRouteWindow / 2, 0), n_[i] - kRouteWindow);
-                const int32_t fl = s_fences[base_[i] + max(a - 1, 0)];
-                const int32_t fh = s_fences[base_[i] + min(a + kRouteWindow, n_[i] - 1)];
-                ok_[i] = (a == 0 || fl <= key[i]) && (a + kRouteWindow >= n_[i] || fh > key[i]);
-            }
-            lo_[i] = a;
-        }
+        for (int h = 0; h < kCombineKeys; h += kSide) {
+            int base_[kSide], n_[kSide], lo_[kSide];
+            bool ok_[kSide];
 #pragma unroll
-        for (int st = 8; st >= 1; st >>= 1) {
-#pragma unroll
-            for (int i = 0; i < kCombineKeys; i++) {
-                const int idx = lo_[i] + st - 1;
-                const int32_t f = s_fences[base_[i] + min(idx, max(n_[i] - 1, 0))];
-                if (idx < n_[i] && f <= key[i]) lo_[i] += st;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < kCombineKeys; i++) {
-            if (!ok_[i]) {  // the guess missed (rare): binary search the whole run
-                const int32_t *fz = s_fences + base_[i];
-                int l = 1, h = n_[i];
-                while (l < h) {
-                    const int mid = (l + h) >> 1;
-                    if (fz[mid] <= key[i]) l = mid + 1;
-                    else h = mid;
+            for (int u = 0; u < kSide; u++) {
+                const int i = h + u;
+                const int r = max(fr[i], 0);
+                base_[u] = (int)s_off[r];
+                n_[u] = fr[i] >= 0 ? (int)s_nf[r] : 0;
+                int a = 0;
+                ok_[u] = true;
+                if (n_[u] > kRouteWindow) {
+                    const int g = (int)max(((float)key[i] - s_f0[r]) * s_scale[r], 0.0f);
+                    a = min(max(g - kRouteWindow / 2, 0), n_[u] - kRouteWindow);
+                    const int32_t fl = s_fences[base_[u] + max(a - 1, 0)];
+                    const int32_t fh = s_fences[base_[u] + min(a + kRouteWindow, n_[u] - 1)];
+                    ok_[u] = (a == 0 || fl <= key[i]) && (a + kRouteWindow >= n_[u] || fh > key[i]);
                 }
-                lo_[i] = l;
+                lo_[u] = a;
             }
-            pg[i] = fr[i] >= 0 ? lo_[i] - 1 : -1;
+#pragma unroll
+            for (int st = 8; st >= 1; st >>= 1) {
+#pragma unroll
+                for (int u = 0; u < kSide; u++) {
+                    const int idx = lo_[u] + st - 1;
+                    const int32_t f = s_fences[base_[u] + min(idx, max(n_[u] - 1, 0))];
+                    if (idx < n_[u] && f <= key[h + u]) lo_[u] += st;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kSide; u++) {
+                const int i = h + u;
+                if (!ok_[u]) {  // the guess missed (rare): binary search the whole run
+                    const int32_t *fz = s_fences + base_[u];
+                    int l = 1, hh = n_[u];
+                    while (l < hh) {
+                        const int mid = (l + hh) >> 1;
+                        if (fz[mid] <= key[i]) l = mid + 1;
+                        else hh = mid;
+                    }
+                    lo_[u] = l;
+                }
+                pg[i] = fr[i] >= 0 ? lo_[u] - 1 : -1;
+            }
         }
         // first / page of the live keys
         if (vec_out && tile_keys == TILE_KEYS) {
@@ -1206,8 +1214,7 @@ __global__ void __launch_bounds__(BLOCK) k_probe_combine_route(
         // candidate rows: bytes of the tile's rows that hold keys (whole
         // 64-key words), run r's byte = bit r of the 8 keys' masks
         if (k0 < ((tile_keys + 63) & ~63)) {
-            const uint32_t lo = cand[0] | (cand[1] << 8) | (cand[2] << 16) | (cand[3] << 24);
-            const uint32_t hi = cand[4] | (cand[5] << 8) | (cand[6] << 16) | (cand[7] << 24);
+            const uint32_t lo = cand_lo, hi = cand_hi;
             const size_t byte0 = tile0 / 8 + threadIdx.x;
 #pragma unroll
             for (int r = 0; r < kMaxStack; r++) {

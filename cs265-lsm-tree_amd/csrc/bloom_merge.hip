@@ -279,19 +279,21 @@ __global__ void __launch_bounds__(kCompactBlock) k_compact_write(
 //
 // Partitions: every kKwayS-th entry of every run is a sample; the samples'
 // ranks in the total order (k_kway_split: binary searches over the other
-// runs' samples) pick every kKwayQ-th sample as a partition start, and the
+// runs' samples) pick every q-th sample as a partition start, and the
 // start's position in each run is found by a binary search between two of
-// that run's samples.  A partition holds exactly kKwayQ samples, so at most
-// (kKwayQ + k) * kKwayS entries: it fits one workgroup's LDS whatever the key
-// distribution or duplicates.  k_kway_merge merges a partition's k shares in
+// that run's samples.  A partition holds exactly q samples, so at most
+// (q + k) * kKwayS entries: with q = kKwayCap / kKwayS - k it fits one
+// workgroup's LDS whatever the key distribution or duplicates (q fixed at 8
+// for every k left a fan-in-4 partition half full on average: twice the
+// partitions, each paying the ticket, bounds and look-back latencies).  k_kway_merge merges a partition's k shares in
 // LDS (log2 k rounds of stable merge-path merges, the newer list on the
 // left), flags the kept entries, and places them with a decoupled look-back
 // over the partitions' kept counts (partitions taken in ticket order, so
 // every partition waits only on ones already running).
 // ---------------------------------------------------------------------------
 constexpr int kKwayS = 256;                                    // sample stride
-constexpr int kKwayQ = 8;                                      // samples per partition
-constexpr int kKwayCap = (kKwayQ + kKwayMaxRuns) * kKwayS;     // entries per partition, at most
+constexpr int kKwayCap = 16 * kKwayS;                          // entries per partition, at most
+static_assert(kKwayCap / kKwayS > kKwayMaxRuns, "at least one sample per partition");
 constexpr int kKwayBlock = 512;
 constexpr int kKwayIpt = kKwayCap / kKwayBlock;                // outputs per lane per round
 static_assert(kKwayIpt * kKwayBlock == kKwayCap, "whole outputs per lane");
@@ -301,6 +303,7 @@ struct KwayRuns {
     uint64_t n[kKwayMaxRuns];
     uint64_t soff[kKwayMaxRuns + 1];  // run r's samples at skeys[soff[r] .. soff[r + 1])
     int k;
+    uint32_t q;  // samples per partition (kway_q)
 };
 
 __global__ void __launch_bounds__(256) k_kway_samples(KwayRuns R, int32_t *__restrict__ skeys) {
@@ -317,7 +320,7 @@ __device__ __forceinline__ bool kway_before(int32_t key, int32_t x, int rr, int 
     return key < x || (key == x && rr < r);
 }
 
-// Thread per sample: its rank; a rank that is a multiple of kKwayQ starts a
+// Thread per sample: its rank; a rank that is a multiple of R.q starts a
 // partition, whose bounds in every run this thread writes.
 __global__ void __launch_bounds__(256) k_kway_split(KwayRuns R, const int32_t *__restrict__ skeys,
                                                    uint32_t *__restrict__ bounds, uint32_t nparts) {
@@ -358,8 +361,8 @@ __global__ void __launch_bounds__(256) k_kway_split(KwayRuns R, const int32_t *_
 #pragma unroll
     for (int rr = 0; rr < kKwayMaxRuns; rr++)
         if (rr < k && rr != r) rank += lo[rr];
-    if (rank == 0 || rank % kKwayQ != 0) return;
-    const uint64_t p = rank / kKwayQ;
+    if (rank == 0 || rank % R.q != 0) return;
+    const uint64_t p = rank / R.q;
     // the partition start's position in run rr: c samples of rr come before
     // it, so it lies in ((c - 1) * S, c * S]; a lower bound in that window
     uint32_t a[kKwayMaxRuns], b[kKwayMaxRuns];
@@ -687,10 +690,14 @@ hipError_t launch_dedup(const void *in, uint64_t n, int drop_tombstones, void *o
 
 namespace bloomhip {
 
+namespace {
+uint32_t kway_q(int k) { return (uint32_t)(kKwayCap / kKwayS - k); }
+}  // namespace
+
 uint64_t kway_parts(const uint64_t *n, int k) {
     uint64_t ns = 0;
     for (int r = 0; r < k; r++) ns += (n[r] + kKwayS - 1) / kKwayS;
-    return ns ? (ns - 1) / kKwayQ + 1 : 0;
+    return ns ? (ns - 1) / kway_q(k) + 1 : 0;
 }
 
 uint64_t kway_workspace_bytes(const uint64_t *n, int k) {
@@ -707,6 +714,7 @@ hipError_t launch_compact_kway(const void *const *runs, const uint64_t *n, int k
     if (k < 1 || k > kKwayMaxRuns) return hipErrorInvalidValue;
     KwayRuns R{};
     R.k = k;
+    R.q = kway_q(k);
     uint64_t ns = 0;
     for (int r = 0; r < k; r++) {
         if (n[r] == 0 || (reinterpret_cast<uintptr_t>(runs[r]) & 7)) return hipErrorInvalidValue;

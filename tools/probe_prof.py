@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """C3 probe (16.8M GETs x 5 level filters) repeated under one strategy, for
 rocprofv3 --kernel-trace --stats: `python tools/probe_prof.py [auto|stacked|
-partition|gather] [reps]`."""
+partition|gather|route] [reps]` (route: the C3 GET routing, bloomhip_route_gets,
+over runs built with their fences)."""
 import os
 import sys
 
@@ -19,7 +20,8 @@ from bloomhip import workloads as W  # noqa: E402
 def main():
     kind = sys.argv[1] if len(sys.argv) > 1 else "auto"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
-    st = {"auto": bh.PROBE_AUTO, "stacked": bh.PROBE_STACKED, "partition": bh.PROBE_PARTITION,
+    route = kind == "route"
+    st = {"auto": bh.PROBE_AUTO, "route": bh.PROBE_AUTO, "stacked": bh.PROBE_STACKED, "partition": bh.PROBE_PARTITION,
           "gather": bh.PROBE_GATHER}[kind]
     torch.cuda.set_device(0)
     gets, levels = W.c3()
@@ -27,13 +29,21 @@ def main():
     filters = []
     for lvl, keys, m in levels:
         f = bh.BloomFilter(m)
-        f.set_batch(keys)
+        if route:
+            f.set_batch_run(keys)
+        else:
+            f.set_batch(keys)
         f.set_probe_strategy(st)
         filters.append(f)
     out = torch.empty((len(filters), (gets.size + 63) // 64), dtype=torch.int64, device="cuda")
     s = torch.cuda.current_stream()
+    fr = torch.empty(gets.size, dtype=torch.int32, device="cuda")
+    pg = torch.empty(gets.size, dtype=torch.int32, device="cuda")
     for _ in range(reps):
-        bh.test_batch(filters, dgets, out=out, stream=s)
+        if route:
+            bh.route_gets(filters, dgets, cand=out, first=fr, page=pg, stream=s)
+        else:
+            bh.test_batch(filters, dgets, out=out, stream=s)
     torch.cuda.synchronize()
     print("done", kind, reps)
 
