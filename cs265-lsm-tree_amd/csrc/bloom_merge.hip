@@ -491,8 +491,12 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
     while (ABL != 2 && nl > 1) {
         const int np = (nl + 1) / 2;
         // this lane's outputs of the round, into registers: one merge-path
-        // search where the lane enters a pair, then a sequential merge
-        int a0 = 0, a1 = 0, b1 = -1, ia = 0, ib = 0;
+        // search where the lane enters a pair, then a sequential merge with
+        // both lists' head entries held in registers (one 8-B LDS read per
+        // output, for the entry that replaces the one taken; reading both
+        // heads' keys and then the taken entry per output was three)
+        int a1 = 0, b1 = -1, ia = 0, ib = 0;
+        Entry ea{0, 0}, eb{0, 0};
 #pragma unroll
         for (int i = 0; i < kKwayIpt; i++) {
             const int d = d0 + i;
@@ -501,7 +505,7 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
                     // the pair holding output d (pairs are consecutive output ranges)
                     int q = 0;
                     while (q + 1 < np && (int)ofs[min(2 * (q + 1), nl)] <= d) q++;
-                    a0 = (int)ofs[2 * q];
+                    const int a0 = (int)ofs[2 * q];
                     a1 = (int)ofs[min(2 * q + 1, nl)];
                     b1 = (int)ofs[min(2 * q + 2, nl)];
                     const int na = a1 - a0, nb = b1 - a1, dd = d - a0;
@@ -514,9 +518,15 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
                     }
                     ia = a0 + lo;       // absolute LDS indices of the next A and B entries
                     ib = a1 + dd - lo;
+                    ea = s_buf[min(ia, kKwayCap - 1)];  // past a list's end: never taken
+                    eb = s_buf[min(ib, kKwayCap - 1)];
                 }
-                const bool take_a = ia < a1 && (ib >= b1 || s_buf[ia].key <= s_buf[ib].key);
-                mine[i] = take_a ? s_buf[ia++] : s_buf[ib++];
+                const bool take_a = ia < a1 && (ib >= b1 || ea.key <= eb.key);
+                mine[i] = take_a ? ea : eb;
+                const int nx = take_a ? ++ia : ++ib;
+                const Entry e = s_buf[min(nx, kKwayCap - 1)];
+                if (take_a) ea = e;
+                else eb = e;
             }
         }
         __syncthreads();  // every lane's reads of this round's lists and bounds
