@@ -43,6 +43,6 @@ constexpr int kKwayMaxRuns = 8;
 uint64_t kway_workspace_bytes(const uint64_t *n, int k);
 hipError_t launch_compact_kway(const void *const *runs, const uint64_t *n, int k, int drop,
                                void *out, int32_t *keys_out, void *ws, uint32_t *count_out,
-                               hipStream_t stream, int abl = 0);
+                               hipStream_t stream);
 
 }  // namespace bloomhip

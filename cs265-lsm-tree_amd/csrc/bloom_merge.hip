@@ -398,8 +398,10 @@ constexpr uint64_t kKwayAgg = 1ull << 62, kKwayIncl = 2ull << 62, kKwayVal = (1u
 // merge round's outputs are computed into registers (kKwayIpt entries per
 // lane), then written back over the round's input after a barrier, so a
 // workgroup takes 32 KiB and four fit a CU (two buffers halved that: the
-// kernel is latency-bound, 8192 partitions at fan-in 4 x 4M).
-template <int ABL>
+// kernel is latency-bound).  Persistent workgroups that took the next ticket
+// and loaded the next bounds during a partition's merge were slower (292 us
+// against 221 at fan-in 4, rocprofv3): they spilled at 4 workgroups per CU,
+// and a workgroup held in the look-back held its later partitions too.
 __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
     KwayRuns R, const uint32_t *__restrict__ bounds, uint32_t nparts, int drop,
     uint64_t *__restrict__ status, uint32_t *__restrict__ ticket, Entry *__restrict__ out,
@@ -414,7 +416,7 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
     __shared__ int32_t s_pred;
     __shared__ int s_has_pred;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = R.k;
-    if (tid == 0) s_p = (ABL == 5 || ABL >= 7) ? blockIdx.x : atomicAdd(ticket, 1u);  // ticket order: predecessors are running
+    if (tid == 0) s_p = atomicAdd(ticket, 1u);  // ticket order: predecessors are running
     __syncthreads();
     const uint32_t p = s_p;
     // the shares and the entry just before the partition (its predecessor):
@@ -454,7 +456,7 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
             const int d = tid + i * kKwayBlock;
             if (d < total) {
                 while ((int)s_off[r + 1] <= d) r++;
-                mine[i] = ABL == 3 ? Entry{d, d} : R.run[r][s_lo[r] + (uint32_t)(d - (int)s_off[r])];
+                mine[i] = R.run[r][s_lo[r] + (uint32_t)(d - (int)s_off[r])];
             }
         }
     }
@@ -488,7 +490,7 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
     // array indexed by the lane's pair went to scratch memory.
     const uint32_t *ofs = s_off;
     int nl = k;
-    while (ABL != 2 && nl > 1) {
+    while (nl > 1) {
         const int np = (nl + 1) / 2;
         // this lane's outputs of the round, into registers: one merge-path
         // search where the lane enters a pair, then a sequential merge with
@@ -560,9 +562,7 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
     // 8 dependent steps to cross the 512 partitions running at once); the
     // nearest inclusive prefix ends it.  Relaxed agent-scope atomics (only
     // the counts travel).
-    if (ABL == 1 || ABL >= 7) {
-        if (tid == 0) s_base = (uint64_t)p * kKwayCap;
-    } else if (p == 0) {
+    if (p == 0) {
         if (tid == 0) {
             __hip_atomic_store(&status[0], kKwayIncl | ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_base = 0;
@@ -621,7 +621,7 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
             s_base = base;
         }
     }
-    if (tid == 0 && p + 1 == nparts && !(ABL == 1 || ABL >= 7)) *count_out = (uint32_t)(s_base + ctot);
+    if (tid == 0 && p + 1 == nparts) *count_out = (uint32_t)(s_base + ctot);
     __syncthreads();  // every lane's reads of s_buf above are done
     // kept entries packed in place in LDS (they only move down), then written out coalesced
     uint32_t w = excl;
@@ -630,7 +630,7 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
         if ((keep >> i) & 1u) s_buf[w++] = mine[i];
     __syncthreads();
     const uint64_t base = s_base;
-    for (int i = tid; i < ((ABL == 6 || ABL == 8) ? 0 : (int)ctot); i += kKwayBlock) {
+    for (int i = tid; i < (int)ctot; i += kKwayBlock) {
         const Entry e = s_buf[i];
         out[base + i] = e;
         if (keys_out) keys_out[base + i] = e.key;
@@ -720,7 +720,7 @@ uint64_t kway_workspace_bytes(const uint64_t *n, int k) {
 
 hipError_t launch_compact_kway(const void *const *runs, const uint64_t *n, int k, int drop,
                                void *out, int32_t *keys_out, void *ws, uint32_t *count_out,
-                               hipStream_t stream, int abl) {
+                               hipStream_t stream) {
     if (k < 1 || k > kKwayMaxRuns) return hipErrorInvalidValue;
     KwayRuns R{};
     R.k = k;
@@ -749,10 +749,8 @@ hipError_t launch_compact_kway(const void *const *runs, const uint64_t *n, int k
     const unsigned gs = (unsigned)((ns + 255) / 256);
     k_kway_samples<<<gs, 256, 0, stream>>>(R, skeys);
     k_kway_split<<<gs, 256, 0, stream>>>(R, skeys, bounds, (uint32_t)np);
-#define KW(A) k_kway_merge<A><<<(unsigned)np, kKwayBlock, 0, stream>>>(R, bounds, (uint32_t)np, drop, status, \
-        ticket, reinterpret_cast<Entry *>(out), keys_out, count_out)
-    if (abl == 1) KW(1); else if (abl == 2) KW(2); else if (abl == 3) KW(3); else if (abl == 4) {}
-    else if (abl == 5) KW(5); else if (abl == 6) KW(6); else if (abl == 7) KW(7); else if (abl == 8) KW(8); else KW(0);
+    k_kway_merge<<<(unsigned)np, kKwayBlock, 0, stream>>>(R, bounds, (uint32_t)np, drop, status, ticket,
+                                                  reinterpret_cast<Entry *>(out), keys_out, count_out);
     return hipGetLastError();
 }
 

@@ -325,16 +325,6 @@ extern "C" int ubench_ladder_geometry(int nf, const uint64_t *ms, uint64_t *out6
     return 0;
 }
 
-// Diagnosis of the one-pass k-way compaction (temporary): abl 0 product,
-// 1 no look-back (partition p writes at p * cap), 2 no merge rounds, 3 no
-// staging loads, 4 samples + split only.
-extern "C" int ubench_kway(int abl, const void *const *runs, const uint64_t *n, int k, void *out,
-                           int32_t *keys_out, void *ws, uint32_t *count, void *stream) {
-    return launch_compact_kway(runs, n, k, 1, out, keys_out, ws, count,
-                               reinterpret_cast<hipStream_t>(stream), abl) == hipSuccess ? 0 : -5;
-}
-extern "C" uint64_t ubench_kway_ws(const uint64_t *n, int k) { return kway_workspace_bytes(n, k); }
-
 // ---- rocprofv3 counter calibration (tools/ubench.py cal) --------------------
 // Kernels that request a known number of bytes in the access shapes the
 // product issues, so FETCH_SIZE / WRITE_SIZE can be read against them
