@@ -1052,13 +1052,10 @@ int bloomhip_is_set(const bloomhip_filter *fc, int32_t key, int *hit_out) {
     const auto t0 = std::chrono::steady_clock::now();
     while (*hv == 2u && std::chrono::steady_clock::now() - t0 < kIsSetSpin) {
     }
-    if (*hv == 2u) {
-        HIP_TRY(hipStreamSynchronize(s));
-    } else {
-        // the answer arrived: report a launch or kernel error the spin skipped
-        const hipError_t qe = hipStreamQuery(s);
-        if (qe != hipSuccess && qe != hipErrorNotReady) return fail_hip(qe, "k_is_set1");
-    }
+    // (A hipStreamQuery after a successful spin, to report a kernel fault at
+    // once, took the call from 7.7 to 12.0 us median; a fault is sticky and
+    // surfaces at the next synchronising call on this filter instead.)
+    if (*hv == 2u) HIP_TRY(hipStreamSynchronize(s));
     const uint32_t v = *hv;
     if (v > 1u) return fail_hip(hipErrorUnknown, "k_is_set1 result not visible");
     *hit_out = (int)v;
