@@ -212,6 +212,8 @@ struct Workspace {
     size_t mkeys_bytes = 0;
     void *kway = nullptr;  // one-pass compaction: samples, partition bounds, look-back state
     size_t kway_bytes = 0;
+    uint32_t *h_kept = nullptr;  // one-pass compaction: kept count, pinned + mapped (coherent)
+    uint32_t *d_kept = nullptr;  // its device address
 };
 
 std::mutex g_ws_mu;
@@ -253,6 +255,8 @@ void free_workspace_buffers(int device, hipStream_t s, Workspace *w) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
+    if (w->h_kept) (void)hipHostFree(w->h_kept);
+    w->h_kept = w->d_kept = nullptr;
     w->pos_bytes = w->runs_bytes = w->res_bytes = w->slots_bytes = 0;
     w->mbuf_bytes[0] = w->mbuf_bytes[1] = w->msplit_bytes = w->mcount_bytes = w->mkeys_bytes = 0;
     w->kway_bytes = 0;
@@ -1231,6 +1235,8 @@ int bloomhip_trim(void) {
     return BLOOMHIP_OK;
 }
 
+constexpr uint32_t kKeptPending = 0xFFFFFFFFu;  // never a count: total < 2^32 - 1
+
 int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
                      int runs_on_device, int drop_tombstones, void *out_entries, size_t *n_out,
                      int out_on_device, bloomhip_filter *f, int device, void *stream) {
@@ -1292,14 +1298,31 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
                 rn[r] = list[r].second;
             }
             HIP_TRY(grow_touched(&w->kway, &w->kway_bytes, kway_workspace_bytes(rn, k), s));
+            if (!w->h_kept) {
+                HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&w->h_kept), 64,
+                                      hipHostMallocMapped | hipHostMallocCoherent));
+                HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&w->d_kept), w->h_kept, 0));
+            }
+            volatile uint32_t *hk = w->h_kept;
+            *hk = kKeptPending;  // overwritten by the merge's last partition
             void *dst = out_on_device ? out_entries : w->mbuf[1];
             hipError_t e = launch_compact_kway(rp, rn, k, drop_tombstones, dst, f ? w->mkeys : nullptr,
-                                               w->kway, w->mcount, s);
+                                               w->kway, w->d_kept, s);
             if (e != hipSuccess) return fail_hip(e, "k-way compaction launch");
-            uint32_t cnt = 0;
-            HIP_TRY(hipMemcpyAsync(&cnt, w->mcount, 4, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipStreamSynchronize(s));
-            kept = cnt;
+            // The kept count sizes the filter build.  The last partition
+            // stores it (system scope) once every kept count before it is
+            // known, while the merge may still be writing entries: the build
+            // is enqueued on the same stream, so it runs after the merge
+            // anyway, and the GPU does not idle through a copy + synchronise
+            // round trip (0.457 ms per bench call with it).  After 1 s
+            // without the word, the stream is synchronised (which also
+            // reports a failed kernel).
+            const auto t0 = std::chrono::steady_clock::now();
+            while (*hk == kKeptPending && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(1)) {
+            }
+            if (*hk == kKeptPending) HIP_TRY(hipStreamSynchronize(s));
+            kept = *hk;
+            if (kept > total) return fail_hip(hipErrorUnknown, "k-way compaction count not visible");
             if (f) {
                 int rc = kept ? set_batch_run_locked(f, w->mkeys, (size_t)kept, 4, 1, s, true)
                               : set_batch_run_locked(f, dst, 0, 8, 1, s, true);

@@ -306,8 +306,14 @@ struct KwayRuns {
     uint32_t q;  // samples per partition (kway_q)
 };
 
-__global__ void __launch_bounds__(256) k_kway_samples(KwayRuns R, int32_t *__restrict__ skeys) {
+// Also zeroes the look-back state and the ticket (np <= samples: a launch
+// of its own cost more than the stores).
+__global__ void __launch_bounds__(256) k_kway_samples(KwayRuns R, int32_t *__restrict__ skeys,
+                                                      uint64_t *__restrict__ status, uint32_t np,
+                                                      uint32_t *__restrict__ ticket) {
     const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g < np) status[g] = 0;
+    if (g == 0) *ticket = 0;
     if (g >= R.soff[R.k]) return;
     int r = 0;
     while (r + 1 < R.k && R.soff[r + 1] <= g) r++;
@@ -621,7 +627,10 @@ __global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
             s_base = base;
         }
     }
-    if (tid == 0 && p + 1 == nparts) *count_out = (uint32_t)(s_base + ctot);
+    // system scope: the host may spin on this word (pinned, mapped) to size
+    // the next launch before the merge has drained
+    if (tid == 0 && p + 1 == nparts)
+        __hip_atomic_store(count_out, (uint32_t)(s_base + ctot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();  // every lane's reads of s_buf above are done
     // kept entries packed in place in LDS (they only move down), then written out coalesced
     uint32_t w = excl;
@@ -744,10 +753,9 @@ hipError_t launch_compact_kway(const void *const *runs, const uint64_t *n, int k
     b = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(b) + 15) & ~(uintptr_t)15);
     uint64_t *status = reinterpret_cast<uint64_t *>(b);
     uint32_t *ticket = reinterpret_cast<uint32_t *>(status + np);
-    hipError_t e = hipMemsetAsync(status, 0, np * 8 + 4, stream);
-    if (e != hipSuccess) return e;
     const unsigned gs = (unsigned)((ns + 255) / 256);
-    k_kway_samples<<<gs, 256, 0, stream>>>(R, skeys);
+    if ((uint64_t)gs * 256 < np) return hipErrorInvalidValue;  // the samples launch zeroes status
+    k_kway_samples<<<gs, 256, 0, stream>>>(R, skeys, status, (uint32_t)np, ticket);
     k_kway_split<<<gs, 256, 0, stream>>>(R, skeys, bounds, (uint32_t)np);
     k_kway_merge<<<(unsigned)np, kKwayBlock, 0, stream>>>(R, bounds, (uint32_t)np, drop, status, ticket,
                                                   reinterpret_cast<Entry *>(out), keys_out, count_out);
