@@ -542,8 +542,16 @@ int device_cu_count() {
 static bool seg_magic(uint32_t g, uint32_t nsub, uint32_t *magic) {
     if (g == 0) return false;
     const uint32_t M = (uint32_t)(((1ull << 31) + g - 1) / g);
-    for (uint32_t x = 0; x < 2 * nsub; x++)
-        if ((uint32_t)(((uint64_t)x * M) >> 32) != (x >> 1) / g) return false;
+    // x M / 2^32 = x / 2g + x e / (g 2^32) with e = M g - 2^31 < g: the floor
+    // is x / 2g's whenever x e < 2^31 (the fraction of x / 2g is at most
+    // 1 - 1/2g).  Every planned geometry passes that bound; the loop (one
+    // division per value, ~80 us per plan at 2 nsub = 32768, on the host path
+    // of every partition call) is only the fallback.
+    const uint64_t e = (uint64_t)M * g - (1ull << 31);
+    if (nsub && (2ull * nsub - 1) * e >= (1ull << 31)) {
+        for (uint32_t x = 0; x < 2 * nsub; x++)
+            if ((uint32_t)(((uint64_t)x * M) >> 32) != (x >> 1) / g) return false;
+    }
     *magic = M;
     return true;
 }
@@ -724,8 +732,12 @@ bool plan_ladder(const uint64_t *m, int nf, int ncu, StackTable *st, PartitionWo
                 const uint32_t nb1 = L.nblk[1];
                 const uint32_t M = (uint32_t)(((1ull << 32) + nb1 - 1) / nb1);
                 bool exact = nb1 < (1u << 23);
-                for (uint32_t hi = 0; exact && hi < L.ne; hi++)
-                    exact = (uint32_t)(((uint64_t)hi * M) >> 32) == hi / nb1;
+                // exact for hi e < 2^32, e = M nb1 - 2^32 < nb1 (as seg_magic's
+                // bound); the loop only when that bound does not cover ne
+                const uint64_t e = (uint64_t)M * nb1 - (1ull << 32);
+                if (exact && L.ne && (uint64_t)(L.ne - 1) * e >= (1ull << 32))
+                    for (uint32_t hi = 0; exact && hi < L.ne; hi++)
+                        exact = (uint32_t)(((uint64_t)hi * M) >> 32) == hi / nb1;
                 if (!exact) continue;
                 L.ctup = 1;
                 L.tmagic = M;

@@ -271,3 +271,24 @@ def test_digest_covers_every_kernel_source():
                if p.endswith((".hip", ".h"))}
     assert product <= set(listed), product - set(listed)
     assert "bloom_capi.cpp" in listed
+
+
+@pytest.mark.parametrize("shift", [31, 32])
+def test_planner_magic_bound_implies_exact(shift):
+    """The planners (bloom_kernels.hip seg_magic, plan_ladder's computed
+    tuple) skip their exhaustive check of a multiply-high divisor when
+    x * e < 2^shift for every x they divide (M = ceil(2^shift / g),
+    e = M g - 2^shift): the bound is checked here against brute force over
+    every x it admits, for random and edge divisors."""
+    rng = np.random.default_rng(7)
+    gs = [1, 2, 3, 5, 7, 640, 4095, 4096, 40961, (1 << 20) - 1] + list(rng.integers(1, 1 << 22, 40))
+    for g in gs:
+        g = int(g)
+        M = ((1 << shift) + g - 1) // g
+        e = M * g - (1 << shift)
+        xmax = (1 << shift) // e if e else 1 << 22  # x e < 2^shift for x < xmax
+        xmax = min(xmax, 1 << 22)
+        x = np.arange(xmax, dtype=np.uint64)
+        got = (x * np.uint64(M)) >> np.uint64(32)
+        want = x // np.uint64(2 * g) if shift == 31 else x // np.uint64(g)
+        assert np.array_equal(got, want), g
