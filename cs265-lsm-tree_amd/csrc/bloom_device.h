@@ -1059,6 +1059,11 @@ __device__ __forceinline__ int route_page(const int32_t *fz, int n, int32_t k, f
 // rows leave range-checked -- the rows are not written by the combine and
 // read back by k_route.  Persistent workgroups stage the runs' fences once.
 // Member j is run rows.row[j]; the RouteTable is indexed by run.
+// The fused page search's window: 7 fences and 3 halving steps (one
+// dependent LDS read fewer than k_route's 15; the guess from the run's first
+// and last fence lands within a fence or two for C3's keys).
+constexpr int kFusedWindow = 7;
+
 template <int TILE_KEYS, int BLOCK, int LAYOUT>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) k_probe_combine_route(
     const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, KeySpan ks,
@@ -1156,17 +1161,17 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
                 n_[u] = fr[i] >= 0 ? (int)s_nf[r] : 0;
                 int a = 0;
                 ok_[u] = true;
-                if (n_[u] > kRouteWindow) {
+                if (n_[u] > kFusedWindow) {
                     const int g = (int)max(((float)key[i] - s_f0[r]) * s_scale[r], 0.0f);
-                    a = min(max(g - kRouteWindow / 2, 0), n_[u] - kRouteWindow);
+                    a = min(max(g - kFusedWindow / 2, 0), n_[u] - kFusedWindow);
                     const int32_t fl = s_fences[base_[u] + max(a - 1, 0)];
-                    const int32_t fh = s_fences[base_[u] + min(a + kRouteWindow, n_[u] - 1)];
-                    ok_[u] = (a == 0 || fl <= key[i]) && (a + kRouteWindow >= n_[u] || fh > key[i]);
+                    const int32_t fh = s_fences[base_[u] + min(a + kFusedWindow, n_[u] - 1)];
+                    ok_[u] = (a == 0 || fl <= key[i]) && (a + kFusedWindow >= n_[u] || fh > key[i]);
                 }
                 lo_[u] = a;
             }
 #pragma unroll
-            for (int st = 8; st >= 1; st >>= 1) {
+            for (int st = (kFusedWindow + 1) / 2; st >= 1; st >>= 1) {
 #pragma unroll
                 for (int u = 0; u < kSide; u++) {
                     const int idx = lo_[u] + st - 1;
