@@ -2,7 +2,8 @@
 # Runs named GPU steps in order on the box, each under its own time limit,
 # stopping at the first failure (no retries).  Logs: gpurun_out/<tag>/<step>.log
 # Usage: tools/gpu_steps.sh TAG step[,step...]
-#   steps: pytest smoke bench bench_c4 bench_c5 stats_c2 stats_c3 pmc_c2 pmc_c4 pmc_c5
+#   steps: pytest smoke bench bench_c4 bench_c5 stats_c2 stats_c3 stats_c4 stats_c5
+#          stats_route stats_compact pmc_c2 pmc_c3 pmc_c4 pmc_c5 (and the experiments below)
 set -o pipefail
 TAG=${1:?tag}; STEPS=${2:?steps}
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
@@ -61,6 +62,7 @@ for s in ${STEPS//,/ }; do
     stats_compact) run stats_compact 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_compact" -o run --output-format csv -- python tools/compact_prof.py 40 || exit 1 ;;
     stats_compact_alt) run stats_compact_alt 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_compact_alt" -o run --output-format csv -- python tools/compact_prof.py 40 alt || exit 1 ;;
     stats_c3_alt) run stats_c3_alt 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3_alt" -o run --output-format csv -- python tools/probe_prof.py auto 30 alt || exit 1 ;;
+    stats_route) run stats_route 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_route" -o run --output-format csv -- python tools/probe_prof.py route 30 || exit 1 ;;
     stats_c3) run stats_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3" -o run --output-format csv -- python tools/probe_prof.py auto 30 || exit 1 ;;
     pmc_c2) pmc c2 FETCH_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
             pmc c2 WRITE_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
