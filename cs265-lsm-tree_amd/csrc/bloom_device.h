@@ -1089,11 +1089,36 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
         s_scale[r] = (n > 1 && fl > f0) ? (float)(n - 1) / ((float)fl - (float)f0) : 0.0f;
         s_run_of[r] = rows.row[r];
     }
-    for (int r = 0; r < nf; r++) {
-        const uint32_t n = rt.nfences[r];
-        const int32_t *src = rt.meta[r] + 1;
-        int32_t *dst = s_fences + rt.fence_off[r];
-        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) dst[i] = src[i];
+    {
+        // every run's fences, contiguous in LDS (fence_off is the prefix of
+        // the counts), 8 loads in flight per thread (a load-then-store loop
+        // per run waited for each load: ~12 us before the first tile)
+        constexpr int kBatch = 8;
+        const uint32_t total = rt.total_fences;
+        for (uint32_t b = 0; b < total; b += kBatch * BLOCK) {
+            int32_t v[kBatch];
+#pragma unroll
+            for (int q = 0; q < kBatch; q++) {
+                const uint32_t g = b + q * BLOCK + threadIdx.x;
+                // g's run, by compile-time indices (a runtime index into the
+                // kernel-argument arrays went through scratch memory)
+                const int32_t *src = rt.meta[0] + 1;
+                uint32_t off = 0;
+#pragma unroll
+                for (int rr = 1; rr < kMaxStack; rr++) {
+                    if (rr < nf && rt.fence_off[rr] <= g) {
+                        src = rt.meta[rr] + 1;
+                        off = rt.fence_off[rr];
+                    }
+                }
+                v[q] = g < total ? src[g - off] : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < kBatch; q++) {
+                const uint32_t g = b + q * BLOCK + threadIdx.x;
+                if (g < total) s_fences[g] = v[q];
+            }
+        }
     }
     const int k0 = kCombineKeys * (int)threadIdx.x;  // this thread's first key in a tile
     const bool vec_out = ((reinterpret_cast<uintptr_t>(first) | reinterpret_cast<uintptr_t>(page)) & 15) == 0;
@@ -1114,8 +1139,17 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
                 key[i] = k0 + i < tile_keys ? load_key<LAYOUT>(ks, tile0 + k0 + i) : 0;
         }
         __syncthreads();  // the previous tile's result bytes are no longer read
+        // the tile's result bytes: every load issued before any LDS store (a
+        // load-store loop waited for each; loaded before the barrier, they
+        // spilled under the 64-VGPR cap), clamped so no load sits under a branch
+        constexpr int kResVec = kTilePos / 16, kResPer = (kResVec + BLOCK - 1) / BLOCK;
         const uint4 *src = reinterpret_cast<const uint4 *>(res + tile * (size_t)kTilePos);
-        for (int q = threadIdx.x; q < kTilePos / 16; q += BLOCK) reinterpret_cast<uint4 *>(s_r)[q] = src[q];
+        uint4 rv[kResPer];
+#pragma unroll
+        for (int j = 0; j < kResPer; j++) rv[j] = src[min((int)threadIdx.x + j * BLOCK, kResVec - 1)];
+#pragma unroll
+        for (int j = 0; j < kResPer; j++)
+            if ((int)threadIdx.x + j * BLOCK < kResVec) reinterpret_cast<uint4 *>(s_r)[threadIdx.x + j * BLOCK] = rv[j];
         __syncthreads();
         const uint32_t a[4] = {va.x, va.y, va.z, va.w}, b[4] = {vb.x, vb.y, vb.z, vb.w},
                        c[4] = {vc.x, vc.y, vc.z, vc.w};
