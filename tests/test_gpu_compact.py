@@ -149,3 +149,19 @@ def test_compact_more_runs_than_one_pass_takes(coracle, drop):
     want = coracle.compact(runs, drop)
     assert np.array_equal(got, want)
     assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()
+
+
+@pytest.mark.parametrize("k", range(1, 9))
+def test_compact_every_fan_in_of_the_one_pass_kernel(coracle, k):
+    # the one-pass kernel sizes its partitions by the fan-in (q = 16 - k
+    # samples of 256 entries each): every k it takes, with repeated keys
+    # inside and across runs, both tombstone modes, and the fused filter
+    runs = _dup_runs([60_000 + 777 * r for r in range(k)], 40_000, 31 * k)
+    total = sum(r.shape[0] for r in runs)
+    for drop in (False, True):
+        f = bh.BloomFilter(bh.m_bits(total, 10.0))
+        got = bh.compact(runs, drop_tombstones=drop, filter=f)
+        want = coracle.compact(runs, drop)
+        assert np.array_equal(got, want)
+        if want.shape[0]:
+            assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()
