@@ -292,9 +292,9 @@ __global__ void __launch_bounds__(kCompactBlock) k_compact_write(
 // every partition waits only on ones already running).
 // ---------------------------------------------------------------------------
 constexpr int kKwayS = 256;                                    // sample stride
-constexpr int kKwayCap = 16 * kKwayS;                          // entries per partition, at most
+constexpr int kKwayCap = 32 * kKwayS;                          // entries per partition, at most (64 KiB)
 static_assert(kKwayCap / kKwayS > kKwayMaxRuns, "at least one sample per partition");
-constexpr int kKwayBlock = 512;
+constexpr int kKwayBlock = 1024;
 constexpr int kKwayIpt = kKwayCap / kKwayBlock;                // outputs per lane per round
 static_assert(kKwayIpt * kKwayBlock == kKwayCap, "whole outputs per lane");
 
@@ -403,12 +403,15 @@ constexpr uint64_t kKwayAgg = 1ull << 62, kKwayIncl = 2ull << 62, kKwayVal = (1u
 // One workgroup per partition (taken in ticket order).  One LDS buffer: each
 // merge round's outputs are computed into registers (kKwayIpt entries per
 // lane), then written back over the round's input after a barrier, so a
-// workgroup takes 32 KiB and four fit a CU (two buffers halved that: the
-// kernel is latency-bound).  Persistent workgroups that took the next ticket
+// 1024-lane workgroup takes 64 KiB and two fit a CU (two buffers halved
+// that: the kernel is latency-bound).  Partitions of up to 8192 entries on
+// 1024 lanes: 189 us at fan-in 4 against 210 for 4096 on 512 lanes (four per
+// CU; each partition pays the ticket, its bounds and the look-back) and 260
+// for 16384 on 1024 lanes (one per CU).  Persistent workgroups that took the next ticket
 // and loaded the next bounds during a partition's merge were slower (292 us
 // against 221 at fan-in 4, rocprofv3): they spilled at 4 workgroups per CU,
 // and a workgroup held in the look-back held its later partitions too.
-__global__ void __launch_bounds__(kKwayBlock, 4) k_kway_merge(
+__global__ void __launch_bounds__(kKwayBlock, 2) k_kway_merge(
     KwayRuns R, const uint32_t *__restrict__ bounds, uint32_t nparts, int drop,
     uint64_t *__restrict__ status, uint32_t *__restrict__ ticket, Entry *__restrict__ out,
     int32_t *__restrict__ keys_out, uint32_t *__restrict__ count_out) {
