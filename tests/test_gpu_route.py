@@ -238,3 +238,40 @@ def test_route_fused_into_stacked_combine(coracle, layout):
         cand, first, page = dc.cpu().numpy().view(np.uint64), df.cpu().numpy(), dp.cpu().numpy()
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     assert not cand[1].any() and (first >= 0).sum() > 1000
+
+
+def test_route_fused_duplicate_fences_and_edges(coracle):
+    """The fused routing (one ladder stack, STACKED) on runs whose fences
+    repeat (long stretches of equal keys: upper_bound must pass them all),
+    a run clustered in a narrow range next to one spread over all of int32
+    (page guesses off by many fences), and GETs at, just below and just above
+    every fence plus both int32 extremes."""
+    rng = np.random.default_rng(41)
+    sizes = [4096, 16_384, 65_536, 262_144]
+    small = np.sort(rng.integers(-1000, 1000, size=sizes[0], dtype=np.int64)).astype(np.int32)
+    dup = np.sort(np.repeat(rng.integers(-2**31, 2**31, size=sizes[1] // 4096, dtype=np.int64),
+                            4096)).astype(np.int32)
+    clustered = np.sort(np.concatenate([
+        rng.integers(0, 50_000, size=sizes[2] - 300, dtype=np.int64),
+        rng.integers(-2**31, 2**31, size=300, dtype=np.int64)])).astype(np.int32)
+    spread = sorted_run(sizes[3], 5)
+    runs, refs = [], []
+    for keys in (small, dup, clustered, spread):
+        assert keys.size in sizes
+        m = bh.m_bits(keys.size, 10.0)
+        f = bh.BloomFilter(m)
+        f.set_probe_strategy(bh.PROBE_STACKED)
+        f.set_batch_run(keys)
+        runs.append(f)
+        refs.append((keys, m))
+    fences = np.concatenate([k[::4096] for k, _ in refs]).astype(np.int64)
+    edge = np.clip(np.concatenate([fences - 1, fences, fences + 1]), -2**31, 2**31 - 1).astype(np.int32)
+    pool = np.concatenate([k for k, _ in refs])
+    gets = np.concatenate([edge, pool[rng.integers(0, pool.size, size=200_000)],
+                           rng.integers(-2**31, 2**31, size=60_000, dtype=np.int64).astype(np.int32),
+                           np.array([np.iinfo(np.int32).min, np.iinfo(np.int32).max], dtype=np.int32)])
+    rng.shuffle(gets)
+    cand, first, page = bh.route_gets(runs, gets)
+    wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
+    assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
+    assert (first == 1).any() and (page[first == 2] > 0).any()
