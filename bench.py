@@ -338,9 +338,14 @@ def route_c3(torch, bh):
     wall, n_pre = time_leg(
         lambda: bh.route_gets(runs, dgets, cand=dc, first=df, page=dp, stream=s), torch)
     routed = int((df >= 0).sum().item())
+    # SURVEY §8(d)'s probe bytes (keys, every filter, a bit per key and run)
+    # plus the routing outputs (first and page: 8 B per key)
+    algo = 4 * n + sum((m + 7) // 8 for _, _, m in levels) + len(runs) * n // 8 + 8 * n
     return {"gkeys_s": round(n / (wall * 1e9), 3), "wall_ms": round(wall * 1e3, 4),
             "timed_calls": LEG_MIN_CALLS, "prewarm_calls": n_pre,
-            "keys_with_candidate": routed}
+            "keys_with_candidate": routed, "algorithmic_bytes": algo,
+            "achieved_GBps": round(algo / wall / 1e9, 1),
+            "frac": round(algo / wall / 1e9 / HBM_PEAK_GBPS, 4)}
 
 
 def probe_c3_sharded(torch, bh, dist, rank, world, coll_dev):
@@ -457,9 +462,12 @@ def compact_fanin(torch, bh):
         f.clear()
         got[0] = bh.compact(druns, drop_tombstones=True, filter=f, out=dout)
     t, n_pre = time_leg(call, torch)
+    n_out = int(got[0].shape[0])
+    algo = 8 * total + 8 * n_out + (m + 7) // 8  # runs in, merged run out, the new filter
     return {"gentries_s": round(total / t / 1e9, 3), "ms": round(t * 1e3, 3),
             "timed_calls": LEG_MIN_CALLS, "prewarm_calls": n_pre,
-            "entries_in": total, "entries_out": int(got[0].shape[0]),
+            "entries_in": total, "entries_out": n_out, "algorithmic_bytes": algo,
+            "achieved_GBps": round(algo / t / 1e9, 1), "frac": round(algo / t / 1e9 / HBM_PEAK_GBPS, 4),
             "note": "4 sorted runs merged newest-wins + tombstones dropped + filter/fences "
                     "of the merged run built; wall clock per synchronous call"}
 
