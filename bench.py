@@ -261,13 +261,15 @@ def load_pins():
         return json.load(f)
 
 
-def probe_c3(torch, bh):
-    """configs[2] / SURVEY §8d C3: 16.8M GETs against the five level filters
-    in one call.  Each level's packed hit row is checked against the oracle's
-    SHA-256 pin (tests/golden/pins.json), not only its hit count."""
+def probe_leg(torch, bh, workload="c3"):
+    """configs[2] / SURVEY §8d C3 (workload "c3"): 16.8M GETs against the five
+    level filters in one call; "f10": the same GETs against the three level
+    filters of the reference's published f = 10 tree (workloads.f10).  Each
+    level's packed hit row is checked against the oracle's SHA-256 pin
+    (tests/golden/pins.json), not only its hit count."""
     import numpy as np
     from bloomhip import workloads as W
-    gets, levels = W.c3()
+    gets, levels = W.c3() if workload == "c3" else W.f10()
     filters = []
     for lvl, keys, m in levels:
         f = bh.BloomFilter(m)
@@ -294,18 +296,19 @@ def probe_c3(torch, bh):
     hit_counts = [int(np.unpackbits(hits[j].view(np.uint8)).sum()) for j in range(len(filters))]
     pins = load_pins()
     sha_ok = None
-    if pins:
-        want = {lv["level"]: lv["hits_sha256"] for lv in pins["oracle"]["c3"]["levels"]}
+    if pins and workload in pins["oracle"]:
+        want = {lv["level"]: lv["hits_sha256"] for lv in pins["oracle"][workload]["levels"]}
         got = {lvl: hashlib.sha256(hits[j].tobytes()).hexdigest()
                for j, (lvl, _, _) in enumerate(levels)}
         sha_ok = got == want
         if not sha_ok:
-            log("probe_c3: HIT ROWS DIFFER from the oracle pins")
+            log(f"probe {workload}: HIT ROWS DIFFER from the oracle pins")
     algo = 4 * gets.size + sum((m + 63) // 64 * 8 for _, _, m in levels) + len(levels) * nw * 8
-    pmc = pmc_traffic("c3")
+    pmc = pmc_traffic(workload) if workload == "c3" else None
     traffic = None if not pmc or pmc.get("stale") else pmc.get("hbm_bytes_per_probe")
     return {"gkeys_s": round(gets.size / (wall * 1e9), 3),
             "kernel_ms": round(kms, 4), "wall_ms": round(wall * 1e3, 4),
+            "levels_m_bits": [m for _, _, m in levels],
             "timed_calls": LEG_MIN_CALLS, "prewarm_calls": n_pre,
             "kernels": {k: round(v["ms"] / LEG_MIN_CALLS, 4) for k, v in prof.items()},
             "algorithmic_bytes": algo,
@@ -316,6 +319,10 @@ def probe_c3(torch, bh):
             "traffic_source": "profiles/pmc_c3.json" if traffic else None,
             "hits_per_level": hit_counts,
             "hits_sha_match": sha_ok}
+
+
+def probe_c3(torch, bh):
+    return probe_leg(torch, bh, "c3")
 
 
 def route_c3(torch, bh):
@@ -472,18 +479,14 @@ def compact_fanin(torch, bh):
                     "of the merged run built; wall clock per synchronous call"}
 
 
-def c4_build(torch, bh, reps=LEG_MIN_CALLS):
-    """configs[3] / SURVEY §8d C4: one run of 268,435,456 keys at 12 bits/key
-    (m = 3,221,225,472 bits, a 384 MiB bitmap: beyond LDS, L2 and most of
-    the Infinity Cache).  The bitmap is checked against the oracle's SHA-256
-    pin; the device time per build comes from HIP events on the launch stream
-    around `reps` back-to-back builds (after a time-based prewarm), the
-    roofline from (4N + m/8) per build, traffic from profiles/pmc_c4.json."""
-    from bloomhip import workloads as W
-    keys, m = W.c4()
+def build_leg(torch, bh, keys, m, pin_sha, traffic_workload=None, reps=LEG_MIN_CALLS):
+    """One device-resident build of `keys` into m bits, repeated: the bitmap
+    is checked against the oracle's SHA-256 pin; the device time per build
+    comes from HIP events on the launch stream around `reps` back-to-back
+    builds (after a time-based prewarm), the roofline from (4N + m/8) per
+    build, traffic from profiles/pmc_<traffic_workload>.json."""
     n = keys.size
     dk = torch.from_numpy(keys).cuda()
-    del keys
     f = bh.BloomFilter(m)
     s = torch.cuda.current_stream()
 
@@ -492,12 +495,11 @@ def c4_build(torch, bh, reps=LEG_MIN_CALLS):
         f.set_batch(dk, stream=s)
     step()
     torch.cuda.synchronize()
-    pins = load_pins()
     ok = None
-    if pins:
-        ok = hashlib.sha256(f.words().tobytes()).hexdigest() == pins["oracle"]["c4"]["sha256"]
+    if pin_sha:
+        ok = hashlib.sha256(f.words().tobytes()).hexdigest() == pin_sha
         if not ok:
-            log("c4_build: BITMAP MISMATCH vs oracle fixture")
+            log(f"build of {n} keys into m={m}: BITMAP MISMATCH vs oracle fixture")
     time_leg(step, torch, calls=0)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
@@ -518,7 +520,7 @@ def c4_build(torch, bh, reps=LEG_MIN_CALLS):
     f.profile(False)
     algo = 4 * n + (m + 63) // 64 * 8
     achieved = algo / (dev_ms * 1e-3) / 1e9
-    pmc = pmc_traffic("c4")
+    pmc = pmc_traffic(traffic_workload) if traffic_workload else None
     traffic = None if not pmc or pmc.get("stale") else pmc.get("hbm_bytes_per_build")
     out = {"gkeys_s": round(n / (dev_ms * 1e-3) / 1e9, 3), "device_ms": round(dev_ms, 4),
            "wall_ms": round(wall * 1e3, 4), "builds_timed": reps,
@@ -528,13 +530,42 @@ def c4_build(torch, bh, reps=LEG_MIN_CALLS):
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                         "traffic": traffic,
                         "traffic_ratio": round(traffic / algo, 2) if traffic else None,
-                        "traffic_source": "profiles/pmc_c4.json" if traffic else None,
+                        "traffic_source": f"profiles/pmc_{traffic_workload}.json" if traffic else None,
                         "algorithmic_bytes": algo},
            "verified_vs_oracle": ok}
     del dk, f
+    return out
+
+
+def c4_build(torch, bh, reps=LEG_MIN_CALLS):
+    """configs[3] / SURVEY §8d C4: one run of 268,435,456 keys at 12 bits/key
+    (m = 3,221,225,472 bits, a 384 MiB bitmap: beyond LDS, L2 and most of
+    the Infinity Cache), checked against its oracle pin (build_leg)."""
+    from bloomhip import workloads as W
+    keys, m = W.c4()
+    pins = load_pins()
+    out = build_leg(torch, bh, keys, m, pins["oracle"]["c4"]["sha256"] if pins else None,
+                    traffic_workload="c4", reps=reps)
     bh.lib().bloomhip_trim()  # the 3 GB partition workspace of this size
     torch.cuda.empty_cache()
     return out
+
+
+def f10_legs(torch, bh):
+    """The reference's own published tree (b = 1000, f = 10, at -r 10:
+    doc/final/final.tex:195-212, src/main.cpp:89, src/lsm_tree.cpp:36-41,
+    workloads F10): level sizes m = 5,120,000 * 10^i bits, whose odd part
+    625 * 5^i takes none of the p2 / ladder paths that C2-C5 (d | 255) take.
+    A build of 16.8M keys into level 2's filter (m = 512,000,000) and the
+    16.8M C3-style GETs against levels 0..2, each checked against its pin."""
+    from bloomhip import workloads as W
+    keys, m = W.f10_build()
+    pins = load_pins()
+    pin = pins["oracle"].get("f10") if pins else None
+    return {"build": build_leg(torch, bh, keys, m, pin["build"]["sha256"] if pin else None),
+            "probe": probe_leg(torch, bh, "f10"),
+            "note": "reference's published tree b=1000 f=10 at 10 bits/entry: "
+                    "m_i = 5,120,000*10^i (odd part 625*5^i)"}
 
 
 def c1_check(bh):
@@ -836,6 +867,8 @@ def main():
             extras["c4_build"] = c4_build(torch, bh)
         log("probe C3 ...")
         extras["probe_c3"] = probe_c3(torch, bh)
+        log("f = 10 tree ...")
+        extras["f10"] = f10_legs(torch, bh)
         log("route C3 ...")
         extras["route_c3"] = route_c3(torch, bh)
         log("compact ...")
@@ -927,6 +960,8 @@ def main():
         "c3_hits_sha": (extras.get("probe_c3") or {}).get("hits_sha_match"),
         "c4_bitmap_sha": (extras.get("c4_build") or {}).get("verified_vs_oracle"),
         "c5_eight_bitmaps_sha": (extras.get("c5_eight_runs") or {}).get("verified_vs_oracle"),
+        "f10_build_bitmap_sha": ((extras.get("f10") or {}).get("build") or {}).get("verified_vs_oracle"),
+        "f10_hits_sha": ((extras.get("f10") or {}).get("probe") or {}).get("hits_sha_match"),
     }
     print(json.dumps(line), flush=True)
     if dist:

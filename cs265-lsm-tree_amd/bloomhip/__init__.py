@@ -46,7 +46,7 @@ PROBE_LDS = 3
 PROBE_STACKED = 4
 STRATEGY_NAMES = {BUILD_AUTO: "auto", BUILD_ATOMIC: "atomic", BUILD_LDS: "lds",
                   BUILD_PARTITION: "partition"}
-PROF_SLOTS = 10
+PROF_SLOTS = 12
 
 # Every symbol include/bloomhip.h and include/bloomhip_workload.h declare.
 EXPORTED_SYMBOLS = (

@@ -15,6 +15,14 @@ C3  generator --puts 22347776 --gets 16777216 --gets-skewness 0.2
     65,536.  Every GET probes all five filters.
 C4  one run of 268,435,456 keys, 12 bits/key.
 C5  runs r = 0..7 of 67,108,864 keys each (generator seed 13141 + r), 10 bits/key.
+F10 the reference's own published tree (doc/final/final.tex:195-212: b = 1000,
+    t = 4, f = 10) at -r 10: the buffer holds 1000*4096/8 = 512,000 entries
+    (src/main.cpp:89), level i one run of capacity 512,000*10^i
+    (src/lsm_tree.cpp:36-41), so m_i = 5,120,000*10^i bits (src/run.cpp:15):
+    15625 << 15 for level 2 -- an odd part 625*5^i, which no d | 255 p2 or
+    ladder path covers.  f10_build: 16,777,216 keys into level 2's filter
+    (m = 512,000,000); f10: 16.8M GETs (skew 0.2, misses 0.3, as C3) against
+    full runs of levels 0..2.
 
 k = 3 everywhere: the reference has three fixed hashes and no k parameter
 (src/bloom_filter.h:8-10), so config 2's "k=7" is not expressible bit-exactly.
@@ -38,6 +46,11 @@ C4_N = 268_435_456
 C4_BPE = 12.0
 C5_N = 67_108_864
 C5_RUNS = 8
+F10_BUFFER = 1000 * 4096 // 8   # -b 1000: buffer_max_entries, src/main.cpp:89
+F10_FANOUT = 10
+F10_LEVELS = 3
+F10_BPE = 10.0
+F10_BUILD_N = 16_777_216
 
 
 def c1_run(n_puts: int = 100_000, buffer_entries: int = 51_200, seed: int = SEED):
@@ -109,3 +122,29 @@ def c4(seed: int = SEED, n: int = C4_N):
 
 def c5_run(r: int, n: int = C5_N):
     return gen_puts(SEED + r, n), m_bits(n, 10.0)
+
+
+def f10_caps():
+    return [F10_BUFFER * F10_FANOUT ** i for i in range(F10_LEVELS)]
+
+
+def f10_build(seed: int = SEED, n: int = F10_BUILD_N):
+    """(keys, m): a run of n keys into the filter of the f = 10 tree's level 2
+    (m = m_bits(51,200,000, 10.0) = 512,000,000 = 15625 << 15)."""
+    return gen_puts(seed, n), m_bits(f10_caps()[2], F10_BPE)
+
+
+def f10(seed: int = SEED):
+    """(gets, [(level, keys, m) for level 0..2]) for the f = 10 tree: full runs
+    of capacity 512,000 * 10^i (oldest, largest first in the put stream, as
+    c3), 16.8M GETs at skew 0.2 / misses 0.3."""
+    caps = f10_caps()
+    puts, gets = gen_workload(seed, sum(caps), C3_GETS, 0.2, 0.3)
+    levels = []
+    start = 0
+    for lvl in reversed(range(F10_LEVELS)):
+        cap = caps[lvl]
+        levels.append((lvl, puts[start:start + cap], m_bits(cap, F10_BPE)))
+        start += cap
+    levels.sort(key=lambda t: t[0])
+    return gets, levels

@@ -73,10 +73,13 @@ enum ProfSlot {
     SLOT_COPY = 7,
     SLOT_PROBE_LDS = 8,
     SLOT_PROBE_STACK = 9,
+    SLOT_PROBE_STACK_ROUTE = 10,  // a stacked probe with GET routing fused into its combine
+    SLOT_ROUTE = 11,              // k_route after the probes (routing not fused)
 };
 const char *kSlotNames[BLOOMHIP_PROF_SLOTS] = {
     "clear(memset)", "k_build_atomic", "k_build_lds",       "k_part_bin", "k_part_apply",
     "k_probe",       "probe_partitioned", "copy",           "k_probe_lds",  "probe_stacked",
+    "probe_stacked+route", "k_route",
 };
 
 struct PendingTiming {
@@ -829,7 +832,7 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
         // in its combine (k_probe_combine_route), not in k_route afterwards
         const bool fuse = route && (int)mem.size() == nf && route->rt->nruns == nf &&
                           (size_t)route->rt->total_fences * 4 <= kRouteLdsFenceBytes;
-        hipError_t e = timed(f0, SLOT_PROBE_STACK, s, [&] {
+        hipError_t e = timed(f0, fuse ? SLOT_PROBE_STACK_ROUTE : SLOT_PROBE_STACK, s, [&] {
             return fuse ? launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s,
                                                route->rt, route->first, route->page)
                         : launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s);
@@ -999,7 +1002,8 @@ int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const voi
     rc = probe_rows(f0, runs, nruns, ks, n, dcand, s, &fr);
     if (rc) return rc;
     if (!fr.routed) {  // the filters were probed apart: route over their rows
-        hipError_t e = launch_route(ks, t, dcand, nw, dfirst, dpage, s);
+        hipError_t e = timed(f0, SLOT_ROUTE, s,
+                             [&] { return launch_route(ks, t, dcand, nw, dfirst, dpage, s); });
         if (e != hipSuccess) return fail_hip(e, "k_route launch");
     }
     if (!out_on_device) {
@@ -1054,8 +1058,7 @@ int bloomhip_is_set(const bloomhip_filter *fc, int32_t key, int *hit_out) {
     constexpr std::chrono::microseconds kIsSetSpin{1000};
     volatile uint32_t *hv = reinterpret_cast<volatile uint32_t *>(f->h_hit);
     const auto t0 = std::chrono::steady_clock::now();
-    while (*hv == 2u && std::chrono::steady_clock::now() - t0 < kIsSetSpin) {
-    }
+    while (*hv == 2u && std::chrono::steady_clock::now() - t0 < kIsSetSpin) __builtin_ia32_pause();
     // (A hipStreamQuery after a successful spin, to report a kernel fault at
     // once, made the call 12.0 us median against 8.7 without it, bench
     // scalar_is_set; a fault is sticky and surfaces at the next synchronising
@@ -1314,12 +1317,15 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
             // known, while the merge may still be writing entries: the build
             // is enqueued on the same stream, so it runs after the merge
             // anyway, and the GPU does not idle through a copy + synchronise
-            // round trip (0.457 ms per bench call with it).  After 1 s
-            // without the word, the stream is synchronised (which also
-            // reports a failed kernel).
+            // round trip (0.457 ms per bench call with it).  The spin is
+            // bounded (kKeptSpin, with a pause per poll): when the stream has
+            // more queued ahead of the merge than that, the stream is
+            // synchronised instead of holding a core (this also reports a
+            // failed kernel).
+            constexpr std::chrono::microseconds kKeptSpin{2000};
             const auto t0 = std::chrono::steady_clock::now();
-            while (*hk == kKeptPending && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(1)) {
-            }
+            while (*hk == kKeptPending && std::chrono::steady_clock::now() - t0 < kKeptSpin)
+                __builtin_ia32_pause();
             if (*hk == kKeptPending) HIP_TRY(hipStreamSynchronize(s));
             kept = *hk;
             if (kept > total) return fail_hip(hipErrorUnknown, "k-way compaction count not visible");

@@ -190,6 +190,60 @@ constexpr uint32_t kBinShift = 19;  // 8192 segments << 19 < 2^32
 // runs[tile * nbins + b], for k_runs_transpose (large tables).
 constexpr int kModFast = 0, kModWide = 1, kModP2 = 2, kModLadder = 3, kModLadder0 = 4;
 
+// The bin (segment) of one raw hash and its pass-1 entry (the position's low
+// kEntryBits bits, or the ladder's packed form), by reduction MK: pass 1's
+// whole per-position arithmetic after the hash (tools/ubench.py prices it
+// alone as the compute ceiling of pass 1).
+template <int MK, int MINW>
+__device__ __forceinline__ void bin_entry(uint64_t raw, const ModParams &mp, const SegMap &sm,
+                                          uint32_t &b, uint32_t &ent) {
+    if constexpr (MK == kModWide) {
+        const uint64_t p = mod_wide(raw, mp);
+        b = seg_of(p, sm);
+        ent = (uint32_t)p & kEntryMask;
+    } else if constexpr (MK == kModLadder) {
+        // ladder stack (StackTable::lad): bin = hash bits
+        // [s, s+u), entry = (a_max << hb | bits [s+u, t_max))
+        // << s | bits [0, s) with a_max = (x >> t_max) % d
+        const uint32_t xl = (uint32_t)raw;
+        const uint32_t a = mod_p2_hi(raw, mp);
+        b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
+        const uint32_t ehi =
+            (a << sm.lad_hb) + __builtin_amdgcn_ubfe(xl, sm.scaled_shift, sm.lad_hb);
+        ent = (ehi << sm.shift) | __builtin_amdgcn_ubfe(xl, 0, sm.shift);
+    } else if constexpr (MK == kModLadder0) {
+        // one-member ladder (plan_build): bin = hash bits
+        // [s, t), entry = a << s | bits [0, s)
+        const uint32_t xl = (uint32_t)raw;
+        if constexpr (MINW >= 6) {
+            // at the 80-VGPR cap of three workgroups per CU
+            // the plain form spilled 50 VGPRs
+            const uint32_t lo = __builtin_amdgcn_ubfe(xl, 0, sm.shift);
+            b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
+            ent = lshl_or_s(mod_p2_hi(raw, mp), sm.shift, lo);
+        } else {
+            // (C5's pass 1: 229 us, against 256 for the pinned
+            // form above and for segments)
+            const uint32_t a = mod_p2_hi(raw, mp);
+            b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
+            ent = (a << sm.shift) | __builtin_amdgcn_ubfe(xl, 0, sm.shift);
+        }
+    } else if constexpr (MK == kModP2) {
+        const uint32_t xl = (uint32_t)raw;
+        const uint32_t r = mod_p2_hi(raw, mp);
+        const uint32_t q = (r << sm.p2_hi_shift) |
+                           __builtin_amdgcn_ubfe(xl, sm.shift, sm.p2_hi_shift);
+        b = __umulhi(q, sm.magic);
+        ent = xl & kEntryMask;
+    } else {
+        // the remainder still scaled by 2^l: the entry is a
+        // bit-field of it, and one shift reaches the segment
+        const uint32_t ru = mod_fast_scaled(raw, mp);
+        b = __umulhi(ru >> sm.scaled_shift, sm.magic);
+        ent = __builtin_amdgcn_ubfe(ru, mp.l, kEntryBits);
+    }
+}
+
 template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4>
 __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                                                        uint64_t *__restrict__ pos_out,
@@ -240,52 +294,9 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
 #pragma unroll
                 for (int h = 0; h < 3; h++) {
                     const uint64_t raw = h == 0 ? raw_hash1(k) : h == 1 ? raw_hash2(k) : raw_hash3(k);
-                    uint32_t b;
-                    if constexpr (MK == kModWide) {
-                        const uint64_t p = mod_wide(raw, mp);
-                        b = seg_of(p, sm);
-                        ent[3 * j + h] = (uint32_t)p & kEntryMask;
-                    } else if constexpr (MK == kModLadder) {
-                        // ladder stack (StackTable::lad): bin = hash bits
-                        // [s, s+u), entry = (a_max << hb | bits [s+u, t_max))
-                        // << s | bits [0, s) with a_max = (x >> t_max) % d
-                        const uint32_t xl = (uint32_t)raw;
-                        const uint32_t a = mod_p2_hi(raw, mp);
-                        b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
-                        const uint32_t ehi =
-                            (a << sm.lad_hb) + __builtin_amdgcn_ubfe(xl, sm.scaled_shift, sm.lad_hb);
-                        ent[3 * j + h] = (ehi << sm.shift) | __builtin_amdgcn_ubfe(xl, 0, sm.shift);
-                    } else if constexpr (MK == kModLadder0) {
-                        // one-member ladder (plan_build): bin = hash bits
-                        // [s, t), entry = a << s | bits [0, s)
-                        const uint32_t xl = (uint32_t)raw;
-                        if constexpr (MINW >= 6) {
-                            // at the 80-VGPR cap of three workgroups per CU
-                            // the plain form spilled 50 VGPRs
-                            const uint32_t lo = __builtin_amdgcn_ubfe(xl, 0, sm.shift);
-                            b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
-                            ent[3 * j + h] = lshl_or_s(mod_p2_hi(raw, mp), sm.shift, lo);
-                        } else {
-                            // (C5's pass 1: 229 us, against 256 for the pinned
-                            // form above and for segments)
-                            const uint32_t a = mod_p2_hi(raw, mp);
-                            b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
-                            ent[3 * j + h] = (a << sm.shift) | __builtin_amdgcn_ubfe(xl, 0, sm.shift);
-                        }
-                    } else if constexpr (MK == kModP2) {
-                        const uint32_t xl = (uint32_t)raw;
-                        const uint32_t r = mod_p2_hi(raw, mp);
-                        const uint32_t q = (r << sm.p2_hi_shift) |
-                                           __builtin_amdgcn_ubfe(xl, sm.shift, sm.p2_hi_shift);
-                        b = __umulhi(q, sm.magic);
-                        ent[3 * j + h] = xl & kEntryMask;
-                    } else {
-                        // the remainder still scaled by 2^l: the entry is a
-                        // bit-field of it, and one shift reaches the segment
-                        const uint32_t ru = mod_fast_scaled(raw, mp);
-                        b = __umulhi(ru >> sm.scaled_shift, sm.magic);
-                        ent[3 * j + h] = __builtin_amdgcn_ubfe(ru, mp.l, kEntryBits);
-                    }
+                    uint32_t b, e;
+                    bin_entry<MK, MINW>(raw, mp, sm, b, e);
+                    ent[3 * j + h] = e;
                     br[3 * j + h] = atomicAdd(&s_hist[b], 4u);
                 }
             } else {
@@ -1019,13 +1030,19 @@ __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
 // branchless halving steps find it there; when the check fails, a binary
 // search over the whole run does (exact either way, only slower).
 constexpr int kRouteWindow = 15;  // fences; answers a .. a + 15: 4 halving steps
+// A page guess is clamped to [0, 2^24] in float before it becomes an int
+// (exact in float; a run has < 2^24 fences: n < 2^32 / kFenceStride).
+constexpr float kGuessMax = 16777216.0f;
 
 __device__ __forceinline__ int route_page(const int32_t *fz, int n, int32_t k, float f0, float scale) {
     int a = 0;
     bool ok = true;
     if (n > kRouteWindow) {
         const float gf = ((float)k - f0) * scale;
-        const int g = (int)max(gf, 0.0f);
+        // clamped in float first: a float-to-int conversion out of int range
+        // is undefined (tight fences make the product huge); any guess past
+        // the run's end is clamped to the last window below anyway
+        const int g = (int)fminf(fmaxf(gf, 0.0f), kGuessMax);
         a = min(max(g - kRouteWindow / 2, 0), n - kRouteWindow);
         // the answer is in [a, a + 15] iff fences[a - 1] <= k and
         // fences[a + 15] > k (a window at either end passes that side)
@@ -1196,7 +1213,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
                 int a = 0;
                 ok_[u] = true;
                 if (n_[u] > kFusedWindow) {
-                    const int g = (int)max(((float)key[i] - s_f0[r]) * s_scale[r], 0.0f);
+                    const int g = (int)fminf(fmaxf(((float)key[i] - s_f0[r]) * s_scale[r], 0.0f), kGuessMax);
                     a = min(max(g - kFusedWindow / 2, 0), n_[u] - kFusedWindow);
                     const int32_t fl = s_fences[base_[u] + max(a - 1, 0)];
                     const int32_t fh = s_fences[base_[u] + min(a + kFusedWindow, n_[u] - 1)];
@@ -1346,13 +1363,10 @@ inline bool p2_pass1(const ModParams &mp, const SegMap &sm) {
     return mp.fast && mp.p2 && mp.p2t >= kEntryBits && sm.shift <= mp.p2t && mp.p2t - sm.shift < 32;
 }
 
-template <bool SLOTS, int TB>
-hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
-                         uint16_t *slots, hipStream_t stream) {
-    constexpr int kCap = TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
-    if (ws.nbins > (size_t)kCap) return hipErrorInvalidValue;
-    const bool cols = runs_as_columns(ws);
-    uint32_t *runs = cols ? ws.run_starts : ws.run_rows;
+// Pass 1's reduction kind (kMod*) and segment map for a batch on geometry
+// ws, as k_part_bin is launched with them; -1 when the geometry is not one
+// pass 1 takes.  (tools/ubench.py prices bin_entry with these alone.)
+inline int pass1_plan(const ModParams &mp, const PartitionWorkspace &ws, bool slots, SegMap *out) {
     SegMap sm = seg_map_of(ws);
     const bool wide = !mp.fast;
     if (!wide) {  // the fast path shifts the remainder scaled by 2^l
@@ -1362,52 +1376,70 @@ hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const Partition
             sm.magic = 0;
         }
     }
+    int mk;
+    if (ws.lad_u) {  // ladder stack: bins are hash bits [s, s + u) (plan_ladder)
+        if (!mp.fast || !mp.p2 || sm.shift + sm.lad_u + sm.lad_hb != mp.p2t) return -1;
+        sm.scaled_shift = sm.shift + sm.lad_u;
+        mk = sm.lad_hb == 0 && !slots ? kModLadder0 : kModLadder;  // plan_build's one-member ladder
+    } else if (wide) {
+        mk = kModWide;
+    } else if (p2_pass1(mp, sm)) {
+        sm.p2_hi_shift = mp.p2t - sm.shift;
+        mk = kModP2;
+    } else {
+        mk = kModFast;
+    }
+    *out = sm;
+    return mk;
+}
+
+template <bool SLOTS, int TB, int MK>
+void bin_launch_layout(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                       uint32_t *runs, const SegMap &sm, bool cols, uint16_t *slots,
+                       hipStream_t stream) {
+    constexpr int kCap = TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
     const bool entry16 =
         ks.layout == KEYS_ENTRY && (reinterpret_cast<uintptr_t>(ks.base) & 15) == 0;
-    if (ws.lad_u) {  // ladder stack: bins are hash bits [s, s + u) (plan_ladder)
-        if (!mp.fast || !mp.p2 || sm.shift + sm.lad_u + sm.lad_hb != mp.p2t)
-            return hipErrorInvalidValue;
-        sm.scaled_shift = sm.shift + sm.lad_u;
-        if (sm.lad_hb == 0 && !SLOTS) {  // plan_build's one-member ladder
-            if (ks.layout == KEYS_PACKED)
-                bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModLadder0>(ks, mp, ws, runs, sm, cols, slots, stream);
-            else if (entry16)
-                bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModLadder0>(ks, mp, ws, runs, sm, cols, slots, stream);
-            else
-                bin_launch<KEYS_STRIDED, SLOTS, TB, kModLadder0, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
-        } else if (ks.layout == KEYS_PACKED)
-            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModLadder>(ks, mp, ws, runs, sm, cols, slots, stream);
-        else if (entry16)
-            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModLadder>(ks, mp, ws, runs, sm, cols, slots, stream);
-        else
-            bin_launch<KEYS_STRIDED, SLOTS, TB, kModLadder, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess || cols) return e;
-        return launch_runs_transpose(ws, stream);
-    }
-    const bool p2 = p2_pass1(mp, sm);
-    if (p2) sm.p2_hi_shift = mp.p2t - sm.shift;
-    if (wide) {
+    // only the packed / entry_t fast paths get the small histogram
+    // capacities; strided keys and m >= 2^32 use the largest
+    if constexpr (MK != kModWide) {
         if (ks.layout == KEYS_PACKED)
-            bin_launch<KEYS_PACKED, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
+            bin_launch_fast<KEYS_PACKED, SLOTS, TB, MK>(ks, mp, ws, runs, sm, cols, slots, stream);
         else if (entry16)
-            bin_launch<KEYS_ENTRY, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
+            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, MK>(ks, mp, ws, runs, sm, cols, slots, stream);
         else
-            bin_launch<KEYS_STRIDED, SLOTS, TB, kModWide, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
-    } else if (p2) {
-        if (ks.layout == KEYS_PACKED)
-            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModP2>(ks, mp, ws, runs, sm, cols, slots, stream);
-        else if (entry16)
-            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModP2>(ks, mp, ws, runs, sm, cols, slots, stream);
-        else
-            bin_launch<KEYS_STRIDED, SLOTS, TB, kModP2, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
+            bin_launch<KEYS_STRIDED, SLOTS, TB, MK, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
     } else {
         if (ks.layout == KEYS_PACKED)
-            bin_launch_fast<KEYS_PACKED, SLOTS, TB, kModFast>(ks, mp, ws, runs, sm, cols, slots, stream);
+            bin_launch<KEYS_PACKED, SLOTS, TB, MK, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
         else if (entry16)
-            bin_launch_fast<KEYS_ENTRY, SLOTS, TB, kModFast>(ks, mp, ws, runs, sm, cols, slots, stream);
+            bin_launch<KEYS_ENTRY, SLOTS, TB, MK, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
         else
-            bin_launch<KEYS_STRIDED, SLOTS, TB, kModFast, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
+            bin_launch<KEYS_STRIDED, SLOTS, TB, MK, kCap>(ks, mp, ws, runs, sm, cols, slots, stream);
+    }
+}
+
+template <bool SLOTS, int TB>
+hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                         uint16_t *slots, hipStream_t stream) {
+    constexpr int kCap = TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
+    if (ws.nbins > (size_t)kCap) return hipErrorInvalidValue;
+    const bool cols = runs_as_columns(ws);
+    uint32_t *runs = cols ? ws.run_starts : ws.run_rows;
+    SegMap sm{};
+    switch (pass1_plan(mp, ws, SLOTS, &sm)) {
+        case kModLadder0:
+            if constexpr (!SLOTS) {
+                bin_launch_layout<SLOTS, TB, kModLadder0>(ks, mp, ws, runs, sm, cols, slots, stream);
+                break;
+            } else {
+                return hipErrorInvalidValue;
+            }
+        case kModLadder: bin_launch_layout<SLOTS, TB, kModLadder>(ks, mp, ws, runs, sm, cols, slots, stream); break;
+        case kModWide: bin_launch_layout<SLOTS, TB, kModWide>(ks, mp, ws, runs, sm, cols, slots, stream); break;
+        case kModP2: bin_launch_layout<SLOTS, TB, kModP2>(ks, mp, ws, runs, sm, cols, slots, stream); break;
+        case kModFast: bin_launch_layout<SLOTS, TB, kModFast>(ks, mp, ws, runs, sm, cols, slots, stream); break;
+        default: return hipErrorInvalidValue;
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess || cols) return e;

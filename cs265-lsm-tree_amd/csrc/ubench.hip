@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <numeric>
 
 #include "bloom_device.h"  // the product kernels and launch templates, for ablation builds
 #include "bloom_merge.h"
@@ -61,6 +62,37 @@ __global__ void ub_hash(ModParams mp, int iters, uint32_t *sink) {
     int32_t k = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u);
     for (int i = 0; i < iters; i++) {
         acc ^= mod_fast(raw_hash1(k), mp) + mod_fast(raw_hash2(k), mp) + mod_fast(raw_hash3(k), mp);
+        k += 0x9E3779B9;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// hash3 + the p2 remainder (m = d << t, d | 255: bloom_math.h mod_p2), the
+// remainder the C2-C5 filters take
+__global__ void ub_hash_p2(ModParams mp, int iters, uint32_t *sink) {
+    uint32_t acc = 0;
+    int32_t k = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u);
+    for (int i = 0; i < iters; i++) {
+        acc ^= mod_p2(raw_hash1(k), mp) + mod_p2(raw_hash2(k), mp) + mod_p2(raw_hash3(k), mp);
+        k += 0x9E3779B9;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// Pass 1's whole per-key arithmetic, without its loads, sort or stores: the
+// three hashes and, per hash, the bin and entry exactly as k_part_bin forms
+// them (bin_entry with the product's reduction MK and segment map for the
+// batch's geometry): the VALU ceiling of a build's or probe's pass 1.
+template <int MK>
+__global__ void ub_pass1_arith(ModParams mp, SegMap sm, int iters, uint32_t *sink) {
+    uint32_t acc = 0;
+    int32_t k = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u);
+    for (int i = 0; i < iters; i++) {
+        uint32_t b0, e0, b1, e1, b2, e2;
+        bin_entry<MK, 4>(raw_hash1(k), mp, sm, b0, e0);
+        bin_entry<MK, 4>(raw_hash2(k), mp, sm, b1, e1);
+        bin_entry<MK, 4>(raw_hash3(k), mp, sm, b2, e2);
+        acc ^= (b0 + e0) ^ (b1 + e1) ^ (b2 + e2);
         k += 0x9E3779B9;
     }
     if (acc == 0x12345678u) sink[0] = acc;
@@ -135,6 +167,12 @@ extern "C" int ubench_run(int which, void *dbuf, size_t bytes, uint64_t m, int g
         case 3: ub_lds_or<<<grid, block, 65536, s>>>(iters, sink); break;
         case 4: ub_hash<<<grid, block, 0, s>>>(make_mod_params(m), iters, sink); break;
         case 5: ub_rawhash<<<grid, block, 0, s>>>(iters, sink); break;
+        case 7: {
+            const ModParams mp = make_mod_params(m);
+            if (!mp.p2) return -22;
+            ub_hash_p2<<<grid, block, 0, s>>>(mp, iters, sink);
+            break;
+        }
         case 6: ub_stream<<<grid, block, 0, s>>>(reinterpret_cast<const uint4 *>(dbuf), bytes / 16 - 1, sink); break;
         case 10: case 11: case 12:  // block = waves doing VALU (of 16), iters = hash iters
             ub_mixed<0><<<grid, 1024, 65536, s>>>(make_mod_params(167772160), block, which - 10,
@@ -148,6 +186,42 @@ extern "C" int ubench_run(int which, void *dbuf, size_t bytes, uint64_t m, int g
             ub_mixed<2><<<grid, 1024, 65536, s>>>(make_mod_params(167772160), block, which - 30,
                                                   iters, iters * 6, sink);
             break;
+        default: return -22;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Pass 1's per-key arithmetic (ub_pass1_arith) for the product's geometry:
+// a build of a filter of ms[0] bits (nf = 1, plan_build), or a stacked probe
+// of nf members (plan_ladder, else plan_stack).  *mk_out: the reduction kind.
+extern "C" int ubench_pass1_arith(int nf, const uint64_t *ms, int grid, int block, int iters,
+                                  void *dbuf, void *stream, int *mk_out) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    uint32_t *sink = reinterpret_cast<uint32_t *>(dbuf);
+    PartitionWorkspace ws{};
+    StackTable st{};
+    uint64_t mmax = 0, g = 0, mmin = ~0ull;
+    for (int j = 0; j < nf; j++) {
+        mmax = std::max(mmax, ms[j]);
+        mmin = std::min(mmin, ms[j]);
+        g = g == 0 ? ms[j] : std::gcd(g, ms[j]);
+    }
+    const int ncu = device_cu_count();
+    if (nf == 1) {
+        if (!plan_build(mmax, ncu, &ws)) return -34;
+    } else if (!plan_ladder(ms, nf, ncu, &st, &ws) && !plan_stack(mmax, g, mmin, nf, ncu, &ws)) {
+        return -34;
+    }
+    const ModParams mp = make_mod_params(mmax);
+    SegMap sm{};
+    const int mk = pass1_plan(mp, ws, nf > 1, &sm);
+    *mk_out = mk;
+    switch (mk) {
+        case kModFast: ub_pass1_arith<kModFast><<<grid, block, 0, s>>>(mp, sm, iters, sink); break;
+        case kModWide: ub_pass1_arith<kModWide><<<grid, block, 0, s>>>(mp, sm, iters, sink); break;
+        case kModP2: ub_pass1_arith<kModP2><<<grid, block, 0, s>>>(mp, sm, iters, sink); break;
+        case kModLadder: ub_pass1_arith<kModLadder><<<grid, block, 0, s>>>(mp, sm, iters, sink); break;
+        case kModLadder0: ub_pass1_arith<kModLadder0><<<grid, block, 0, s>>>(mp, sm, iters, sink); break;
         default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;

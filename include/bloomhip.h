@@ -233,7 +233,7 @@ int bloomhip_resolve_strategy(const bloomhip_filter *f, size_t n, int *strategy_
  * is bracketed by HIP events on its stream; bloomhip_profile_read returns,
  * for kernel slot `slot` (0..BLOOMHIP_PROF_SLOTS-1), its name, launch count
  * and summed device milliseconds (it synchronises the stream). */
-#define BLOOMHIP_PROF_SLOTS 10
+#define BLOOMHIP_PROF_SLOTS 12
 int bloomhip_profile_enable(bloomhip_filter *f, int enable);
 int bloomhip_profile_read(bloomhip_filter *f, int slot, const char **name_out,
                           uint64_t *launches_out, double *ms_out);

@@ -14,6 +14,8 @@ Two kinds of vectors live here, kept apart on purpose:
   the GPU box.  ``c1_bitmap.npy`` is the complete C1 bitmap.
 
 Run:  python tests/golden/make_golden.py   (about a minute, ~6 GB RAM)
+      python tests/golden/make_golden.py f10   (adds / refreshes only the
+      f = 10 tree's pins in pins.json, leaving the rest as they are)
 """
 import hashlib
 import json
@@ -67,8 +69,36 @@ def sha(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+def f10_pins(C):
+    """The reference's published tree geometry (workloads F10): the build of
+    16.8M keys into level 2's filter, and each level's filter + hit rows."""
+    kb, mb = W.f10_build()
+    wb = C.build(mb, kb)
+    out = {"build": {"m": mb, "n": int(kb.size), "sha256": sha(wb), "popcount": C.popcount(wb)}}
+    del wb
+    gets, levels = W.f10()
+    out["gets_sha256"] = sha(gets)
+    out["levels"] = []
+    for lvl, keys, m in levels:
+        w = C.build(m, keys)
+        hits = C.test(w, m, gets)
+        out["levels"].append({"level": lvl, "m": m, "n": int(keys.size), "sha256": sha(w),
+                              "popcount": C.popcount(w), "hits_sha256": sha(hits),
+                              "hits": int(np.unpackbits(hits.view(np.uint8)).sum())})
+    return out
+
+
 def main():
     C = COracle()
+    if sys.argv[1:] == ["f10"]:
+        path = os.path.join(HERE, "pins.json")
+        with open(path) as f:
+            pins = json.load(f)
+        pins["oracle"]["f10"] = f10_pins(C)
+        with open(path, "w") as f:
+            json.dump(pins, f, indent=1)
+        print("updated", path)
+        return
     for m, k, a, b, c in KAT:
         assert C.positions([k], m)[0].tolist() == [a, b, c], (m, k)
     for size, bpe, m in M_BITS:
@@ -113,6 +143,7 @@ def main():
         c5.append({"run": r, "m": m5, "n": int(k5.size), "sha256": sha(w5),
                    "popcount": C.popcount(w5)})
     oracle["c5"] = c5
+    oracle["f10"] = f10_pins(C)
 
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump({"source": "SURVEY.md §8a / §0 F4 (compiled reference)",

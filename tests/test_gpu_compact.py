@@ -165,3 +165,26 @@ def test_compact_every_fan_in_of_the_one_pass_kernel(coracle, k):
         assert np.array_equal(got, want)
         if want.shape[0]:
             assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()
+
+
+@pytest.mark.parametrize("repeated", [False, True], ids=["unique", "repeated"])
+def test_compact_large_beyond_one_lookback_window(coracle, repeated):
+    # 4 x 2.6M entries: ~1,450 partitions at fan-in 4, so the merge's
+    # decoupled look-back crosses its 1024-partition window (q0 -= the
+    # window) and partitions wait on predecessors that were not resident
+    # with them (more than the 512 workgroups the chip holds at once); both
+    # tombstone modes, the fused filter and fences, against the oracle
+    sizes = [2_600_000, 2_600_001, 2_599_999, 2_600_003]
+    runs = (_dup_runs(sizes, 3_000_000, 77) if repeated
+            else make_runs(sizes, 2**31 - 1, 78))
+    total = sum(r.shape[0] for r in runs)
+    assert total > 10_000_000
+    for drop in (False, True):
+        f = bh.BloomFilter(bh.m_bits(total, 10.0))
+        got = bh.compact(runs, drop_tombstones=drop, filter=f)
+        want = coracle.compact(runs, drop)
+        assert np.array_equal(got, want)
+        assert (f.words() == coracle.build(f.m, want[:, 0].copy())).all()
+        fences, mk = f.run_meta()
+        wf, wmk = coracle.run_meta(want[:, 0].copy())
+        assert np.array_equal(fences, wf) and mk == wmk

@@ -49,6 +49,7 @@ def torch_cuda():
 # ---------------------------------------------------------------- build ----
 @pytest.mark.parametrize("m", [1, 2, 31, 32, 33, 64, 65, 256, 1000, 65_537, 512_000, 524_288,
                                1_000_003, 4_194_304, 10_485_761, 167_772_160, 671_088_640,
+                               5_120_000, 51_200_000, 512_000_000,  # the f = 10 tree: 625 << 13 ...
                                2**32 - 1, 2**32, 2**32 + 1_000_003, 2**33 - 7])
 @pytest.mark.parametrize("strategy", STRATEGIES, ids=["atomic", "lds", "partition"])
 def test_build_matches_oracle(coracle, m, strategy):
@@ -510,3 +511,39 @@ def test_c5_run0_full_bitmap(golden):
     f = bh.BloomFilter(m)
     f.set_batch(keys)
     assert sha(f.words()) == golden["oracle"]["c5"][0]["sha256"]
+
+
+def test_f10_build_full_bitmap(golden):
+    """The reference's published tree (b = 1000, f = 10, -r 10): 16.8M keys
+    into level 2's filter, m = 512,000,000 = 15625 << 15 (workloads.f10_build),
+    against the oracle's pin, by every build strategy that applies."""
+    from bloomhip import workloads as W
+    keys, m = W.f10_build()
+    pin = golden["oracle"]["f10"]["build"]
+    assert (m, keys.size) == (pin["m"], pin["n"])
+    for strategy in STRATEGIES:
+        f = bh.BloomFilter(m)
+        if not supported(f, strategy):
+            continue
+        f.set_batch(keys)
+        assert sha(f.words()) == pin["sha256"], strategy
+
+
+@pytest.mark.parametrize("probe", [bh.PROBE_AUTO] + PROBES, ids=["auto"] + PROBE_IDS)
+def test_f10_probe_three_levels(golden, probe):
+    """The f = 10 tree's levels 0..2 (m = 5.12M, 51.2M, 512M bits) built from
+    their full runs and probed with the 16.8M GETs in one call: every
+    level's bitmap and hit row against the oracle's pins, per probe kind."""
+    from bloomhip import workloads as W
+    gets, levels = W.f10()
+    pins = golden["oracle"]["f10"]["levels"]
+    filters = []
+    for lvl, keys, m in levels:
+        f = bh.BloomFilter(m)
+        f.set_probe_strategy(probe)
+        f.set_batch(keys)
+        assert sha(f.words()) == pins[lvl]["sha256"], lvl
+        filters.append(f)
+    got = bh.test_batch(filters, gets)
+    for lvl in range(len(levels)):
+        assert sha(got[lvl]) == pins[lvl]["hits_sha256"], lvl

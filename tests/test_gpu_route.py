@@ -90,6 +90,25 @@ def get_keys(refs, n, seed):
     return g
 
 
+def routed_by(runs, call):
+    """Runs call() with profiling on runs[0] (the handle a multi-run call
+    records its launches on) and returns (path, call's result): path is
+    "fused" when the routing ran inside the stacked probe's combine
+    (k_probe_combine_route), "k_route" when k_route ran after the probes."""
+    f0 = runs[0]
+    f0.profile(True)
+    f0.profile_reset()
+    try:
+        out = call()
+        prof = f0.profile_read()
+    finally:
+        f0.profile(False)
+    fused = prof.get("probe_stacked+route", {}).get("launches", 0)
+    plain = prof.get("k_route", {}).get("launches", 0)
+    assert (fused > 0) != (plain > 0), prof
+    return ("fused" if fused else "k_route"), out
+
+
 @pytest.mark.parametrize("probe", [bh.PROBE_AUTO, bh.PROBE_GATHER, bh.PROBE_PARTITION,
                                    bh.PROBE_LDS], ids=["auto", "gather", "partition", "lds"])
 def test_route_matches_oracle(coracle, probe):
@@ -145,7 +164,8 @@ def test_route_many_runs_and_missing_meta(coracle):
     nometa.set_batch(refs[3][0][:5000])           # filter only, no set_batch_run
     runs[12] = nometa
     gets = get_keys(refs, 100_003, 9)
-    cand, first, page = bh.route_gets(runs, gets)
+    path, (cand, first, page) = routed_by(runs, lambda: bh.route_gets(runs, gets))
+    assert path == "k_route"  # 40 runs: no single stack takes them all
     orefs = oracle_runs(coracle, refs)
     orefs[12] = (coracle.build(nometa.m, refs[3][0][:5000]), nometa.m, np.zeros(0, np.int32), 0)
     wc, wf, wp = coracle.route(orefs, gets)
@@ -183,7 +203,8 @@ def test_route_c3_full(coracle, golden):
         runs.append(f)
         fences, mk = coracle.run_meta(keys)
         orefs.append((coracle.build(m, keys), m, fences, mk))
-    cand, first, page = bh.route_gets(runs, gets)
+    path, (cand, first, page) = routed_by(runs, lambda: bh.route_gets(runs, gets))
+    assert path == "fused"  # the five levels are one ladder stack (the bench's route_c3)
     wc, wf, wp = coracle.route(orefs, gets)
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     # filter bits are the pinned C3 probe results restricted by the range check
@@ -223,19 +244,22 @@ def test_route_fused_into_stacked_combine(coracle, layout):
     gets = get_keys(refs, 300_001, 13)
     wc, wf, wp = coracle.route(orefs, gets)
     if layout == "packed":
-        cand, first, page = bh.route_gets(runs, gets)
+        path, (cand, first, page) = routed_by(runs, lambda: bh.route_gets(runs, gets))
     elif layout == "entry":
         aos = np.zeros((gets.size, 2), dtype=np.int32)
         aos[:, 0] = gets
-        cand, first, page = bh.route_gets(runs, aos.reshape(-1), n=gets.size, stride=8)
+        path, (cand, first, page) = routed_by(
+            runs, lambda: bh.route_gets(runs, aos.reshape(-1), n=gets.size, stride=8))
     else:
         n = gets.size
         dc = torch.zeros((len(runs), (n + 63) // 64), dtype=torch.int64, device="cuda")
         df = torch.empty(n, dtype=torch.int32, device="cuda")
         dp = torch.empty(n, dtype=torch.int32, device="cuda")
-        bh.route_gets(runs, torch.from_numpy(gets).cuda(), cand=dc, first=df, page=dp)
+        path, _ = routed_by(runs, lambda: bh.route_gets(runs, torch.from_numpy(gets).cuda(),
+                                                         cand=dc, first=df, page=dp))
         torch.cuda.synchronize()
         cand, first, page = dc.cpu().numpy().view(np.uint64), df.cpu().numpy(), dp.cpu().numpy()
+    assert path == "fused"  # the kernel under test really ran
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     assert not cand[1].any() and (first >= 0).sum() > 1000
 
@@ -271,7 +295,8 @@ def test_route_fused_duplicate_fences_and_edges(coracle):
                            rng.integers(-2**31, 2**31, size=60_000, dtype=np.int64).astype(np.int32),
                            np.array([np.iinfo(np.int32).min, np.iinfo(np.int32).max], dtype=np.int32)])
     rng.shuffle(gets)
-    cand, first, page = bh.route_gets(runs, gets)
+    path, (cand, first, page) = routed_by(runs, lambda: bh.route_gets(runs, gets))
+    assert path == "fused"
     wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     assert (first == 1).any() and (page[first == 2] > 0).any()

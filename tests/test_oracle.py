@@ -107,6 +107,22 @@ def test_c3_pins(coracle, golden):
         assert int(np.unpackbits(hits.view(np.uint8)).sum()) == golden["reference"]["c3_hits"][lvl]
 
 
+def test_f10_level0_pin_by_the_numpy_restatement(golden):
+    """The f = 10 tree's geometry (m = 5,120,000 = 625 << 13: an odd part no
+    p2 form covers) through the independent numpy restatement: level 0's
+    bitmap and its hit row over all 16.8M GETs equal the C oracle's pins."""
+    import hashlib
+    import bloomhip.workloads as W
+    gets, levels = W.f10()
+    lvl, keys, m = levels[0]
+    pin = golden["oracle"]["f10"]["levels"][0]
+    assert (lvl, m, keys.size) == (0, pin["m"], pin["n"]) == (0, 5_120_000, 512_000)
+    w = np_build(m, keys)
+    assert hashlib.sha256(w.tobytes()).hexdigest() == pin["sha256"]
+    hits = pack_bools(np_test_batch(w, m, gets))
+    assert hashlib.sha256(hits.tobytes()).hexdigest() == pin["hits_sha256"]
+
+
 def test_route_restatement_matches_python_loops(coracle):
     """bo_run_meta / bo_route against a direct Python restatement of
     Run::put (src/run.cpp:158-174), Run::get's checks (:94-99) and

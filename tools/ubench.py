@@ -383,6 +383,41 @@ def cal():
                           "known_GBps": round(known / us / 1e3, 1)}), flush=True)
 
 
+LIB.ubench_pass1_arith.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.POINTER(ctypes.c_int)]
+LIB.ubench_pass1_arith.restype = ctypes.c_int
+MK_NAMES = {0: "mod_fast (segments)", 1: "mod_wide (segments)", 2: "p2 (segments)",
+            3: "ladder stack", 4: "ladder build"}
+# the product's geometries: (name, filter sizes); one size = a build, several = a stacked probe
+PASS1_CASES = [("C2 build", [167_772_160]), ("C5 build", [671_088_640]),
+               ("C4 build", [3_221_225_472]), ("C3 probe (5-level ladder)",
+                                               [655_360 * 4 ** i for i in range(4, -1, -1)]),
+               ("f10 build (b=1000, f=10, r=10: m = 15625 << 15)", [512_000_000]),
+               ("f10 probe (3 levels, m = 5.12M * 10^i)", [512_000_000, 51_200_000, 5_120_000])]
+
+
+def pass1_arith(buf, grid, block, iters=256, reps=5):
+    """The compute ceiling of pass 1 per geometry: the three hashes plus the
+    bin and entry of each position, exactly as k_part_bin forms them
+    (ubench_pass1_arith), compute only."""
+    import numpy as np
+    s = torch.cuda.current_stream()
+    for name, sizes in PASS1_CASES:
+        ms_arr = np.array(sizes, dtype=np.uint64)
+        mk = ctypes.c_int(-1)
+        run = lambda: LIB.ubench_pass1_arith(len(sizes), ms_arr.ctypes.data, grid, block, iters,  # noqa: E731
+                                             buf.data_ptr(), s.cuda_stream, ctypes.byref(mk))
+        if run() != 0:
+            print(json.dumps({"op": "pass1 arithmetic", "case": name, "skipped": True}), flush=True)
+            continue
+        ms = _events(run, reps)
+        print(json.dumps({"op": "pass1 arithmetic", "case": name, "m": sizes,
+                          "reduction": MK_NAMES.get(mk.value, mk.value),
+                          "Gkeys_s": round(grid * block * iters / ms / 1e6, 1), "ms": round(ms, 4)}),
+              flush=True)
+
+
 def main():
     torch.cuda.set_device(0)
     if len(sys.argv) > 1 and sys.argv[1] == "mixed":
@@ -431,6 +466,12 @@ def main():
         print(json.dumps({"op": "hash3+mod_fast", "m": m,
                           "Gkeys_s": round(threads * 256 / ms / 1e6, 1), "ms": round(ms, 4)}),
               flush=True)
+    for m in [167_772_160, 671_088_640, 3_221_225_472]:  # C2, C5, C4: m = d << t, d | 255
+        ms = timeit(7, buf, buf.numel() * 4, m, grid, block, 256)
+        print(json.dumps({"op": "hash3+mod_p2", "m": m,
+                          "Gkeys_s": round(threads * 256 / ms / 1e6, 1), "ms": round(ms, 4)}),
+              flush=True)
+    pass1_arith(buf, grid, block)
     ms = timeit(5, buf, buf.numel() * 4, 0, grid, block, 256)
     print(json.dumps({"op": "hash3_raw", "Gkeys_s": round(threads * 256 / ms / 1e6, 1),
                       "ms": round(ms, 4)}), flush=True)
