@@ -59,7 +59,6 @@ constexpr size_t kLdsBitmapBytes = 160 * 1024;
 // workgroup.  plan_segments picks (sub_shift, group) so that the number of
 // segments is a multiple of the CU count: every CU of pass 2 gets the same
 // share.
-constexpr uint32_t kSegMaxBits = 144u * 1024u * 8u;  // 144 KiB of LDS (stacked-probe planes)
 // Pass 2 has no static LDS: segment images may use all 160 KiB (plan_segments).
 constexpr uint32_t kStackMaxBits = 160u * 1024u * 8u;
 constexpr int kPartBlock = 512;
@@ -131,7 +130,7 @@ inline size_t tile_keys_of(const PartitionWorkspace &ws) {
 
 // Geometry of a stacked probe (seg_bits = w): false when no w = g << s with
 // w | m_max, w <= m_min (the smallest member), nf * w bits <= kStackMaxBits
-// and <= kPartMaxBins segments exists.  Prefers the widest w that still
+// and <= kPartMaxBinsBig segments exists.  Prefers the widest w that still
 // gives >= ncu segments.  gcd_m: gcd of the members' sizes (a multiple of
 // 128 bits).
 bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,

@@ -537,18 +537,20 @@ int device_cu_count() {
 }
 
 // The multiply-high divisor of SegMap: magic = ceil(2^31 / g), accepted only
-// when mulhi(x, magic) == (x >> 1) / g for every x < 2 * nsub (checked here,
-// once per plan: nsub <= kPartMaxSub).  g = 1 gives 2^31, i.e. x >> 1.
-static bool seg_magic(uint32_t g, uint32_t nsub, uint32_t *magic) {
-    if (g == 0) return false;
+// when mulhi(x, magic) == (x >> 1) / g for every x < 2 * nsub.  g = 1 gives
+// 2^31, i.e. x >> 1.
+// x M / 2^32 = x / 2g + x e / (g 2^32) with e = M g - 2^31 < g: the floor is
+// x / 2g's whenever x e < 2^31 (the fraction of x / 2g is at most 1 - 1/2g).
+// Every planned geometry passes that bound; the brute-force check (one
+// division per value, ~80 us per plan at 2 nsub = 32768, on the host path of
+// every partition call) is only the fallback, and only over SegMap's
+// original domain (nsub <= kPartMaxSub).
+static bool seg_magic(uint32_t g, uint64_t nsub, uint32_t *magic) {
+    if (g == 0 || nsub == 0 || 2 * nsub > (1ull << 32)) return false;
     const uint32_t M = (uint32_t)(((1ull << 31) + g - 1) / g);
-    // x M / 2^32 = x / 2g + x e / (g 2^32) with e = M g - 2^31 < g: the floor
-    // is x / 2g's whenever x e < 2^31 (the fraction of x / 2g is at most
-    // 1 - 1/2g).  Every planned geometry passes that bound; the loop (one
-    // division per value, ~80 us per plan at 2 nsub = 32768, on the host path
-    // of every partition call) is only the fallback.
     const uint64_t e = (uint64_t)M * g - (1ull << 31);
-    if (nsub && (2ull * nsub - 1) * e >= (1ull << 31)) {
+    if ((2 * nsub - 1) * e >= (1ull << 31)) {
+        if (nsub > kPartMaxSub) return false;
         for (uint32_t x = 0; x < 2 * nsub; x++)
             if ((uint32_t)(((uint64_t)x * M) >> 32) != (x >> 1) / g) return false;
     }
@@ -613,15 +615,18 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
     if (m_max == 0 || m_max > 0xFFFFFFFFull || nf < 1 || nf > kMaxStack || gcd_m == 0 ||
         m_max % gcd_m != 0 || gcd_m % 128 != 0 || m_min < gcd_m)
         return false;
-    // Segment widths w: w | gcd_m, so every member is a whole number of
-    // segments, in at most 144 KiB of images (two pass-2 workgroups per CU
-    // when they fit in 80 KiB).
-    const uint64_t wmax = kSegMaxBits / (uint64_t)nf;
-    uint32_t s0 = 5;
-    while ((((m_max - 1) >> s0) + 1) > kPartMaxBins) s0++;
-    // candidates w = g << s, 128-bit multiples for the 16-B image loads
+    // Segment widths w = g << s: w | m_max, so the segments tile the largest
+    // member, and w <= m_min, so member j's window of a segment, the w bits
+    // from (b * w) mod m_j on, wraps at most once (pass 2 stages it with the
+    // wrap; 128 | m_j keeps every 16-B vector on one side of it); all
+    // members' windows in the pass-2 workgroup's LDS (160 KiB: the kernel
+    // has no static LDS).  The segment map b = mulhi(p >> (s - 1),
+    // ceil(2^31 / g)) must be exact over m_max (seg_magic): any s whose 2^s
+    // divides m_max, so sizes with a large odd part (the f = 10 tree's
+    // 5,120,000 * 10^i = 2^(13+i) * 625 * 5^i) stack too.
+    const uint64_t wmax = kStackMaxBits / (uint64_t)nf;
     uint64_t best_w = 0;
-    uint32_t best_s = 0;
+    uint32_t best_s = 0, best_magic = 0;
     // The segment count sets the run length per tile (tile entries / nbins),
     // w only the LDS image: the widest w that still gives every CU a segment,
     // else (small m_max) the narrowest, for the most segments.
@@ -631,27 +636,26 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
         if (a != b) return a;
         return a ? w > best_w : w < best_w;
     };
-    for (uint32_t s = s0; s < 32 && (1ull << s) <= wmax; s++) {
-        if (gcd_m % (1ull << s)) break;  // larger s cannot divide either
+    for (uint32_t s = 1; s < 32 && (1ull << s) <= wmax; s++) {
+        if (m_max % (1ull << s)) break;  // larger s cannot divide either
         for (uint64_t g = wmax >> s; g >= 1; g--) {
             const uint64_t w = g << s;
-            if (w % 128 || gcd_m % w || w > m_min || m_max / w > kPartMaxBinsBig) continue;
-            if (better(w) || (w == best_w && s > best_s)) {
-                best_w = w;
-                best_s = s;
-            }
+            if (w % 128 || m_max % w || w > m_min || m_max / w > kPartMaxBinsBig) continue;
+            if (!(better(w) || (w == best_w && s > best_s))) continue;
+            uint32_t magic = 0;
+            if (!seg_magic((uint32_t)g, m_max >> s, &magic)) continue;
+            best_w = w;
+            best_s = s;
+            best_magic = magic;
         }
     }
     if (best_w == 0) return false;
-    const uint32_t g = (uint32_t)(best_w >> best_s), nsub = (uint32_t)(m_max >> best_s);
-    uint32_t magic = 0;
-    if (!seg_magic(g, nsub, &magic)) return false;
     ws->sub_shift = best_s;
-    ws->group = g;
-    ws->nsub = nsub;
+    ws->group = (uint32_t)(best_w >> best_s);
+    ws->nsub = (uint32_t)(m_max >> best_s);
     ws->seg_bits = (uint32_t)best_w;
     ws->nbins = (size_t)(m_max / best_w);
-    ws->magic = magic;
+    ws->magic = best_magic;
     return true;
 }
 

@@ -285,7 +285,10 @@ def _stack_case(coracle, ms, probe_keys, strategies=None, stride=4, seed=0):
     [1_000_000, 1_000_000],                       # no 128-bit-multiple w divides 10^6
     [3 * 2**20, 2**20, 3 * 2**18, 2**18, 2**19, 3 * 2**17, 2**17, 2**16, 2**15],  # 9 members
     [5 * 2**21, 2**21, 1_000_003, 5 * 2**19, 2**32 + 15],  # non-divisors, > 2^32 mixed in
-], ids=["c3x64", "c3_l0-3", "pow2", "no_w", "nine", "mixed"])
+    [5_120_000 * 10**i for i in range(3)],        # the f = 10 tree: gcd 625 << 13 (w = 320,000)
+    [256_000 * 10**i for i in range(4)],          # f = 10 at the default r = 0.5: 125 << 11
+    [3**7 * 2**9 * 7**i for i in range(3)],       # odd parts 2187 * 7^i, fanout 7
+], ids=["c3x64", "c3_l0-3", "pow2", "no_w", "nine", "mixed", "f10", "f10_r05", "fan7"])
 def test_stacked_probe_matches_oracle(coracle, ms):
     probe = rand_keys(300_001, 77)
     _stack_case(coracle, ms, probe)
@@ -409,9 +412,12 @@ def test_p2_remainder_every_odd_part(coracle, d, t):
         assert (bh.test_batch([built], probe)[0] == want).all(), (d, t, ps)
 
 
-def test_stacked_probe_profile_slot():
-    """The stacked pass runs (and is timed) when AUTO should pick it."""
-    ms = [655_360 * 4**i for i in range(5)]
+@pytest.mark.parametrize("ms", [[655_360 * 4**i for i in range(5)],
+                                [5_120_000 * 10**i for i in range(3)]], ids=["c3", "f10"])
+def test_stacked_probe_profile_slot(ms):
+    """The stacked pass runs (and is timed) when AUTO should pick it: C3's
+    levels (a ladder) and the f = 10 tree's (a segment stack whose width
+    has a large odd part)."""
     filters = []
     for j, m in enumerate(ms):
         f = bh.BloomFilter(m)
