@@ -709,6 +709,20 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     auto load = [&](int t, uint32_t vi) -> uint4 {
         return reinterpret_cast<const uint4 *>(pos + (size_t)rt(t) * TILE_KEYS)[min(vi, kLastVec)];
     };
+    // The vector a lane loads for its step at vector vi of a run ending at
+    // entry `end`, group base vector vb.  WALK 2 (short runs): a lane whose
+    // vector lies past the run's end loads the group's first vector instead
+    // -- a line the group reads anyway, so the wave instruction touches fewer
+    // distinct lines (C4's ~10-entry runs span 2-3 of a group's 4 vectors:
+    // pass 2 1190 -> 1158 us).  The lane keeps its own vi for the entry
+    // mask, so none of what it loaded counts.  Longer runs keep the plain
+    // load: there the vector past a run's end starts the neighbour
+    // segment's run, which an XCD neighbour reads next from the same L2
+    // (C2 pass 2 35.5 -> 39.5 us with the redirect, profiles/r05/redirect/).
+    auto vload = [&](uint32_t vi, uint32_t vb, uint32_t end) -> uint32_t {
+        if constexpr (WALK == 2) return 6 * vi < end ? vi : vb;
+        return vi;
+    };
     // The six entries of vector vi of tile t; run = [r.x, r.y).
     auto apply6 = [&](const uint4 &v, int t, uint32_t vi, const uint2 &r) {
         const uint32_t e[6] = {v.x & kEntryMask, __builtin_amdgcn_alignbit(v.y, v.x, 21) & kEntryMask,
@@ -851,7 +865,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         }
     };
 
-    if constexpr (WALK == 1) {
+    if constexpr (WALK >= 1) {
         // Independent lane groups: group q (G lanes) walks tiles q, q + Q,
         // q + 2Q, ... one step (G vectors) per iteration, moving to its next
         // tile as soon as its run ends, so no group waits for the longest run
@@ -868,7 +882,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         int t = wave * kGroupsPerWave + tl;
         uint32_t r = bnd(t), rn = bnd(t + Q);
         uint32_t vb = (r & 0xFFFFu) / 6u;  // the group's step base (vector index)
-        uint4 v = load(min(t, ntiles - 1), vb + sub);
+        uint4 v = load(min(t, ntiles - 1), vload(vb + sub, vb, r >> 16));
         while (__ballot(t < ntiles) != 0) {
             // state after this step: advance within the run or to the next
             // tile.  On a tile change the new lookahead bounds are loaded
@@ -885,7 +899,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             }
             uint32_t rn2 = rn;
             if (adv) rn2 = bnd(t2 + Q);
-            const uint4 v2 = load(min(t2, ntiles - 1), vb2 + sub);
+            const uint4 v2 = load(min(t2, ntiles - 1), vload(vb2 + sub, vb2, r2 >> 16));
             if (t < ntiles && 6 * vb < (r >> 16)) apply6(v, t, vb + sub, dec(r));
             t = t2; r = r2; rn = rn2; vb = vb2; v = v2;
         }
@@ -902,7 +916,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             r[d] = dec(rp[d]);
             t[d] = min(j * kBatchTiles + d * kTPI + tl, ntiles - 1);
             vi[d] = r[d].x / 6u + sub;
-            v[d] = load(t[d], vi[d]);
+            v[d] = load(t[d], vload(vi[d], vi[d] - sub, r[d].y));
         }
         uint32_t rn[DEPTH];
         const int jn = j + (BLOCK / 64);
@@ -912,7 +926,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) {
             for (uint32_t vn = r[d].x / 6u + sub + G; __ballot(6 * vn < r[d].y) != 0; vn += G)
-                apply6(load(t[d], vn), t[d], vn, r[d]);
+                apply6(load(t[d], vload(vn, vn - sub, r[d].y)), t[d], vn, r[d]);
         }
 #pragma unroll
         for (int d = 0; d < DEPTH; d++) rp[d] = rn[d];
@@ -1550,15 +1564,21 @@ hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *w
         return launch_ladder_nf<8, TK, 0>(ws, m, res, st, stream);
     } else if constexpr (MODE == kApplyStack) {
         // independent lane groups at G = 4 (C3, 5 levels: 108 -> 102 us; 4 levels: equal)
-        if (apply_lanes_per_tile(ws.nbins, 3 * TK) <= 4)
+        if (apply_lanes_per_tile(ws.nbins, 3 * TK) <= 4) {
+            if (3 * TK / ws.nbins < 24)  // short runs: loads past a run's end redirected
+                return launch_stack_nf<4, TK, 2>(ws, m, res, st, stream);
             return launch_stack_nf<4, TK, 1>(ws, m, res, st, stream);
+        }
         return launch_stack_nf<8, TK>(ws, m, res, st, stream);
     } else {
         switch (apply_lanes_per_tile(ws.nbins, 3 * TK)) {
-            case 4:  // builds: independent lane groups (C2 pass 2 39.5 -> 34.4 us, C4 1.39 -> 1.36 ms)
-                if constexpr (MODE == kApplyBuild || MODE == kApplyBuildL)
+            case 4:  // builds: independent lane groups (C2 pass 2 39.5 -> 34.4 us, C4 1.39 -> 1.36 ms),
+                     // runs shorter than a group's step: loads past a run's end redirected
+                if constexpr (MODE == kApplyBuild || MODE == kApplyBuildL) {
+                    if (3 * TK / ws.nbins < 24)
+                        return launch_apply_g<MODE, 4, TK, 1, 2>(ws, m, words, nw32, merge, res, st, stream);
                     return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
-                else
+                } else
                     return launch_apply_g<MODE, 4, TK>(ws, m, words, nw32, merge, res, st, stream);
             case 8: return launch_apply_g<MODE, 8, TK>(ws, m, words, nw32, merge, res, st, stream);
             case 16: return launch_apply_g<MODE, 16, TK>(ws, m, words, nw32, merge, res, st, stream);

@@ -2,9 +2,12 @@
 """Interleaved A/B of the C3 probe (16.8M GETs x 5 level filters) and the C3
 GET routing between two builds of libbloomhip, in child processes on one
 GPU: A = cs265-lsm-tree_amd/lib_alt (tools/build_alt.sh REV), B = lib/.
+Workload c3 (default) or f10 (the f = 10 tree's three levels; its GETs are
+routed over the three level runs the same way).
 Each child prewarms, then times 50 probe calls (HIP events on the launch
 stream) and 30 routing calls; rounds alternate B A B A so clock drift hits
-both alike.  Usage: python tools/probe_ab.py [rounds]"""
+both alike.
+Usage: python tools/probe_ab.py [rounds] [c3|f10]"""
 import json
 import os
 import subprocess
@@ -18,7 +21,7 @@ sys.path.insert(0, sys.argv[1])
 import torch
 import bloomhip as bh
 from bloomhip import workloads as W
-gets, levels = W.c3()
+gets, levels = W.c3() if sys.argv[2] == "c3" else W.f10()
 dg = torch.from_numpy(gets).cuda()
 fs = []
 for _, keys, m in levels:
@@ -50,6 +53,7 @@ print(json.dumps({"probe_ms": round(p, 4), "route_ms": round(r, 4),
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    workload = sys.argv[2] if len(sys.argv) > 2 else "c3"
     alt = os.path.join(ROOT, "cs265-lsm-tree_amd", "lib_alt", "libbloomhip.so")
     res = {"A": [], "B": []}
     for r in range(rounds):
@@ -58,7 +62,8 @@ def main():
             env.pop("BLOOMHIP_LIB", None)
             if v == "A":
                 env["BLOOMHIP_LIB"] = alt
-            out = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "cs265-lsm-tree_amd")],
+            out = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "cs265-lsm-tree_amd"),
+                                  workload],
                                  env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(out.stderr[-2000:], file=sys.stderr)
