@@ -244,7 +244,9 @@ __device__ __forceinline__ void bin_entry(uint64_t raw, const ModParams &mp, con
     }
 }
 
-template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4>
+// NO_TILE_STORE (micro-benchmarks only): skip the sorted tile's stores.
+template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4,
+          bool NO_TILE_STORE = false>
 __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                                                        uint64_t *__restrict__ pos_out,
                                                        uint32_t *__restrict__ runs, SegMap sm,
@@ -410,8 +412,15 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
             v[r] = make_uint4(lshl_or(e[1], 21, e[0]), lshl_or(e[2], 10, e[1] >> 11),
                               lshl_or(e[4], 21, e[3]), lshl_or(e[5], 10, e[4] >> 11));
         }
+        if constexpr (!NO_TILE_STORE) {
 #pragma unroll
-        for (int r = 0; r < kStores; r++) dst[r * TB + tid] = v[r];
+            for (int r = 0; r < kStores; r++) dst[r * TB + tid] = v[r];
+        } else {
+            // keep the packing: a store only when an impossible value shows
+#pragma unroll
+            for (int r = 0; r < kStores; r++)
+                if (v[r].x == 0xFFFFFFFFu && v[r].y == 0xFFFFFFFFu) dst[r * TB + tid] = v[r];
+        }
     };
 
     // Full tiles in the loop; the short last tile (index ntiles - 1, always
@@ -425,6 +434,285 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
         do_tile(BoolC<true>{}, tile, next);
 #pragma unroll
         for (int j = 0; j < kPartKPT; j++) kcur[j] = knext[j];
+        tile = next;
+    }
+    if (tile < ntiles) do_tile(BoolC<false>{}, tile, ntiles);
+}
+
+// ---------------------------------------------------------------------------
+// pass 1 on super-tiles (k_part_bin2, builds with many short runs: C4): one
+// 1024-thread workgroup sorts a tile of kSuperTileKeys = 16,384 keys, two
+// halves of 8,192 (A, B), so each segment's run of a tile is twice as long
+// as k_part_bin's (C4: ~20 entries against ~10) and there are half as many
+// (tile, segment) pairs for pass 2 to walk and half the run table.  Neither
+// the sorted tile (49,152 entries, 192 KiB as u32) nor every position's
+// entry and rank in registers fit (96 live values per thread spilled ~100
+// VGPRs at the 128 of 4 waves per SIMD), so:
+//   1. A's positions: bin + entry (bin_entry), rank in the JOINT histogram
+//      (the rank atomic's return stays in a register), the key's three
+//      entries packed into one u64 of an LDS stash (64 KiB, the thread's own
+//      column: conflict-free);
+//   2. B's positions: the same, entries kept in registers;
+//   3. one scan of the joint counts: segment b's run of the super-tile is
+//      [off(b), off(b + 1)), written to the run table;
+//   4. every entry's index in the sorted super-tile, f = off(b) + rank (one
+//      LDS read);
+//   5. two phases of 24,576 sorted entries each: the entries whose f falls
+//      in the phase (A's taken from the stash) are written to the 96 KiB LDS
+//      image at f - phase base, which goes out packed as k_part_bin's.
+// The histogram and the scan's wave sums live in the image's space (both
+// are dead before the first phase writes): stash + image = all 160 KiB.
+// Ranks reach 49,151, so the rank field is 18 bits: bins at << 20 (at most
+// 4,095 bins), the bin's byte address is (rank value) >> 18.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBinShift2 = 20;
+constexpr int kSuperBlock = 1024;
+
+template <int LAYOUT>
+__device__ __forceinline__ void load_half_keys(const KeySpan &ks, size_t tile, int half, int tid,
+                                               int32_t (&k)[kPartKPT]) {
+    constexpr size_t kHalf = (size_t)kSuperBlock * kPartKPT;
+    const size_t i0 = tile * kSuperTileKeys + half * kHalf + (size_t)kPartKPT * tid;
+    const bool full = tile * kSuperTileKeys + (half + 1) * kHalf <= ks.n;  // uniform per workgroup
+    if constexpr (LAYOUT == KEYS_PACKED) {
+        if (full) {
+            const int4 *v = reinterpret_cast<const int4 *>(ks.base) + i0 / 4;
+            const int4 a = v[0], b = v[1];
+            k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
+            k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
+            return;
+        }
+    } else if constexpr (LAYOUT == KEYS_ENTRY) {
+        if (full) {
+            const int4 *v = reinterpret_cast<const int4 *>(ks.base) + i0 / 2;
+            const int4 a = v[0], b = v[1], c = v[2], d = v[3];
+            k[0] = a.x; k[1] = a.z; k[2] = b.x; k[3] = b.z;
+            k[4] = c.x; k[5] = c.z; k[6] = d.x; k[7] = d.z;
+            return;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kPartKPT; j++) {
+        const size_t i = i0 + j;
+        k[j] = i < ks.n ? load_key<LAYOUT>(ks, i) : 0;
+    }
+}
+
+template <int LAYOUT, bool COLS, int MK, int MAXB>
+__global__ void __launch_bounds__(kSuperBlock, 4) k_part_bin2(KeySpan ks, ModParams mp,
+                                                              uint64_t *__restrict__ pos_out,
+                                                              uint32_t *__restrict__ runs, SegMap sm,
+                                                              size_t ntiles) {
+    constexpr int TB = kSuperBlock;
+    constexpr int kHalfKeys = TB * kPartKPT;          // 8192
+    constexpr int kTileKeys = 2 * kHalfKeys;          // 16384
+    constexpr int kTilePos = 3 * kTileKeys;           // 49152
+    constexpr int kPhasePos = kTilePos / 2;           // 24576 entries: 96 KiB
+    constexpr uint32_t kPhaseBytes = 4u * kPhasePos;
+    constexpr int kScanPer = (MAXB + 1 + TB - 1) / TB;
+    constexpr int kPer = 3 * kPartKPT;                // positions per thread and half
+    constexpr int kStashWords = 2 * kHalfKeys;        // one u64 per key of half A
+    static_assert(4 * kTilePos <= (1 << 18) && kTilePos < (1 << 16) &&
+                      ((uint64_t)MAXB << kBinShift2) < (1ull << 32),
+                  "rank fields (the bin nbins, never incremented, included)");
+    static_assert(kSuperTileKeys == (size_t)kTileKeys, "super-tile size");
+    static_assert(MAXB + 1 + TB / 64 <= kPhasePos, "histogram and wave sums inside the image");
+    // [stash: kStashWords][image: kPhasePos], histogram + wave sums at the
+    // image's start until the phases
+    __shared__ __attribute__((aligned(16))) uint32_t s_pool[kStashWords + kPhasePos];
+    uint2 *stash = reinterpret_cast<uint2 *>(s_pool);
+    uint32_t *img = s_pool + kStashWords;
+    uint32_t *s_hist = img;
+    uint32_t *s_wsum = img + MAXB + 1;
+    char *img_b = reinterpret_cast<char *>(img);
+    const char *hist_b = reinterpret_cast<const char *>(s_hist);
+
+    const int nb = (int)sm.nbins;
+    const int per = (nb + 1 + TB - 1) / TB;
+    int32_t kA[kPartKPT], kB[kPartKPT];
+
+    auto do_tile = [&](auto full_c, size_t tile, size_t next) {
+        constexpr bool FULL = decltype(full_c)::value;
+        // The thread index, opaque per tile: what derives from it (the scan's
+        // bins and run-table pointers, stash and image addresses) is formed
+        // in the tile, not hoisted out of the tile loop into ~30 registers
+        // that the 128-VGPR cap then spilled.
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, wave = tid >> 6;
+        const size_t tile0 = tile * kTileKeys;
+        const int tile_keys = FULL ? kTileKeys : (int)min((size_t)kTileKeys, ks.n - tile0);
+        auto live = [&](int half, int j) { return FULL || half * kHalfKeys + kPartKPT * tid + j < tile_keys; };
+        // B's keys load under A's hashing (needed only after it)
+        load_half_keys<LAYOUT>(ks, tile, 1, tid, kB);
+        lds_barrier();  // the previous tile's image and stash reads are done
+#pragma clang loop unroll(disable) vectorize(disable)
+        for (int b = tid; b <= nb; b += TB) s_hist[b] = (uint32_t)b << kBinShift2;
+        lds_barrier();
+
+        // 1. A: rank in the joint histogram, the key's entries to the stash
+        uint32_t brA[kPer], brB[kPer], eB[2 * kPartKPT];
+#pragma unroll
+        for (int j = 0; j < kPartKPT; j++) {
+            uint32_t e[3];
+#pragma unroll
+            for (int h = 0; h < 3; h++) {
+                const int q = 3 * j + h;
+                e[h] = 0;
+                if (live(0, j)) {
+                    const uint64_t raw = h == 0 ? raw_hash1(kA[j]) : h == 1 ? raw_hash2(kA[j]) : raw_hash3(kA[j]);
+                    uint32_t b;
+                    bin_entry<MK, 4>(raw, mp, sm, b, e[h]);
+                    brA[q] = atomicAdd(&s_hist[b], 4u);
+                } else {
+                    brA[q] = 0;
+                }
+            }
+            stash[j * TB + tid] = make_uint2(lshl_or(e[1], 21, e[0]), lshl_or(e[2], 10, e[1] >> 11));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // 2. B: the same, the key's entries kept packed (two registers for
+        //    three entries: the unpacked 24 spilled)
+#pragma unroll
+        for (int j = 0; j < kPartKPT; j++) {
+            uint32_t e[3];
+#pragma unroll
+            for (int h = 0; h < 3; h++) {
+                const int q = 3 * j + h;
+                e[h] = 0;
+                if (live(1, j)) {
+                    const uint64_t raw = h == 0 ? raw_hash1(kB[j]) : h == 1 ? raw_hash2(kB[j]) : raw_hash3(kB[j]);
+                    uint32_t b;
+                    bin_entry<MK, 4>(raw, mp, sm, b, e[h]);
+                    brB[q] = atomicAdd(&s_hist[b], 4u);
+                } else {
+                    brB[q] = 0;
+                }
+            }
+            eB[2 * j] = lshl_or(e[1], 21, e[0]);
+            eB[2 * j + 1] = lshl_or(e[2], 10, e[1] >> 11);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        lds_barrier();
+
+        // 3. exclusive scan of the joint counts (k_part_bin step 2)
+        const bool scan_wave = wave * 64 * per <= nb;
+        uint32_t local[kScanPer];
+        uint32_t tsum = 0, incl = 0;
+        if (scan_wave) {
+#pragma unroll
+            for (int q = 0; q < kScanPer; q++) {
+                const int b = tid * per + q;
+                local[q] = (q < per && b <= nb) ? s_hist[b] - ((uint32_t)b << kBinShift2) : 0u;
+                tsum += local[q];
+            }
+            incl = wave_incl_scan(tsum);
+            if (lane == 63) s_wsum[wave] = incl;
+        }
+        lds_barrier();
+        if (scan_wave) {
+            uint32_t run = incl - tsum;
+            for (int w = 0; w < wave; w++) run += s_wsum[w];
+#pragma unroll
+            for (int q = 0; q < kScanPer; q++) {
+                const int b = tid * per + q;
+                if (q < per && b <= nb) {
+                    s_hist[b] = run - ((uint32_t)b << kBinShift2);
+                    const uint32_t pk = (run >> 2) | (((run + local[q]) >> 2) << 16);
+                    if (b < nb) {
+                        if constexpr (COLS) runs[(size_t)b * ntiles + tile] = pk;
+                        else runs[tile * (size_t)nb + b] = pk;
+                    }
+                    run += local[q];
+                }
+            }
+        }
+        lds_barrier();
+        if (next < ntiles) load_half_keys<LAYOUT>(ks, next, 0, tid, kA);
+
+        // 4. every entry's byte slot in the sorted super-tile (dead: ~0, in
+        //    no phase); in groups of 6 (the scheduler would otherwise issue
+        //    all 48 reads first, into 48 more registers)
+#pragma unroll
+        for (int q = 0; q < kPer; q++) {
+            const uint32_t fa = *reinterpret_cast<const uint32_t *>(hist_b + (brA[q] >> 18)) + brA[q];
+            const uint32_t fb = *reinterpret_cast<const uint32_t *>(hist_b + (brB[q] >> 18)) + brB[q];
+            brA[q] = live(0, q / 3) ? fa : ~0u;
+            brB[q] = live(1, q / 3) ? fb : ~0u;
+            // formed here: the compiler otherwise defers the add into both
+            // phases and keeps the read offset and the rank value apart
+            // (two registers per entry instead of one)
+            asm volatile("" : "+v"(brA[q]), "+v"(brB[q]));
+            if (q % 6 == 5) __builtin_amdgcn_sched_barrier(0);
+        }
+        lds_barrier();  // the histogram is read: the image is free
+
+        // 5. two phases of kPhasePos sorted entries through the LDS image
+        uint4 *dst = reinterpret_cast<uint4 *>(pos_out + tile * (size_t)kTileKeys);
+        constexpr int kVecs = kPhasePos / 6;  // 16-B vectors per phase
+        constexpr int kStores = kVecs / TB;
+        static_assert(kStores * TB == kVecs, "whole vectors per thread");
+#pragma unroll
+        for (int ph = 0; ph < 2; ph++) {
+            const uint32_t base = ph * kPhaseBytes;
+            // the stash words of all 8 keys first (one wait), then the
+            // conditional writes: a read inside each branch waited for the
+            // LDS round trip once per entry
+            uint2 w[kPartKPT];
+#pragma unroll
+            for (int j = 0; j < kPartKPT; j++) w[j] = stash[j * TB + tid];
+#pragma unroll
+            for (int j = 0; j < kPartKPT; j++) {
+#pragma unroll
+                for (int h = 0; h < 3; h++) {
+                    const uint32_t la = brA[3 * j + h] - base;
+                    if (la < kPhaseBytes) {
+                        const uint32_t e = h == 0 ? w[j].x & kEntryMask
+                                         : h == 1 ? __builtin_amdgcn_alignbit(w[j].y, w[j].x, 21) & kEntryMask
+                                                  : w[j].y >> 10;
+                        *reinterpret_cast<uint32_t *>(img_b + la) = e;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kPartKPT; j++) {
+#pragma unroll
+                for (int h = 0; h < 3; h++) {
+                    const uint32_t lb = brB[3 * j + h] - base;
+                    if (lb < kPhaseBytes) {
+                        const uint32_t lo = eB[2 * j], hi = eB[2 * j + 1];
+                        const uint32_t e = h == 0 ? lo & kEntryMask
+                                         : h == 1 ? __builtin_amdgcn_alignbit(hi, lo, 21) & kEntryMask
+                                                  : hi >> 10;
+                        *reinterpret_cast<uint32_t *>(img_b + lb) = e;
+                    }
+                }
+            }
+            lds_barrier();
+#pragma unroll
+            for (int r = 0; r < kStores; r++) {
+                const uint2 *src = reinterpret_cast<const uint2 *>(img + 6 * (r * TB + tid));
+                const uint2 a = src[0], b = src[1], c = src[2];
+                uint32_t e[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+                if constexpr (!FULL) {
+#pragma unroll
+                    for (int z = 0; z < 6; z++) e[z] &= kEntryMask;
+                }
+                dst[ph * kVecs + r * TB + tid] =
+                    make_uint4(lshl_or(e[1], 21, e[0]), lshl_or(e[2], 10, e[1] >> 11),
+                               lshl_or(e[4], 21, e[3]), lshl_or(e[5], 10, e[4] >> 11));
+            }
+            if (ph == 0) lds_barrier();  // phase 0's image is read before phase 1 writes
+        }
+    };
+
+    const size_t nfull = ks.n / kTileKeys;
+    size_t tile = part_tile(0, ntiles);
+    if (tile < ntiles) load_half_keys<LAYOUT>(ks, tile, 0, (int)threadIdx.x, kA);
+    size_t round = 0;
+    for (; tile < nfull; round++) {
+        const size_t next = part_tile(round + 1, ntiles);
+        do_tile(BoolC<true>{}, tile, next);
         tile = next;
     }
     if (tile < ntiles) do_tile(BoolC<false>{}, tile, ntiles);
@@ -1311,6 +1599,9 @@ hipError_t launch_bin_build1024(const KeySpan &ks, const ModParams &mp, const Pa
                                 hipStream_t stream);
 hipError_t launch_bin_probe512(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                                uint16_t *slots, hipStream_t stream);
+// pass 1 of a build on super-tiles (bloom_pass1_super.hip)
+hipError_t launch_bin_super(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                            hipStream_t stream);
 hipError_t launch_bin_probe1024(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                                 uint16_t *slots, hipStream_t stream);
 // pass 2 of the probes (bloom_probe.hip, bloom_probe_ladder.hip) and the combine
@@ -1460,6 +1751,43 @@ hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const Partition
     return launch_runs_transpose(ws, stream);
 }
 
+
+// Pass 1 on super-tiles (k_part_bin2): builds whose geometry plan_build gave
+// kSuperTileKeys (segments of m < 2^32, more than kSuperMinBins of them).
+template <int MK>
+hipError_t launch_bin_super_mk(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                               const SegMap &sm, hipStream_t stream) {
+    const bool cols = runs_as_columns(ws);
+    uint32_t *runs = cols ? ws.run_starts : ws.run_rows;
+    const size_t g = (size_t)device_cu_count();
+    const unsigned grid = (unsigned)(ws.ntiles < g ? ws.ntiles : g);
+    const bool entry16 = ks.layout == KEYS_ENTRY && (reinterpret_cast<uintptr_t>(ks.base) & 15) == 0;
+#define SUPER_L(L, C) \
+    k_part_bin2<L, C, MK, (int)kSuperMaxBins><<<grid, kSuperBlock, 0, stream>>>(ks, mp, ws.pos, runs, sm, ws.ntiles)
+    if (ks.layout == KEYS_PACKED) {
+        if (cols) SUPER_L(KEYS_PACKED, true); else SUPER_L(KEYS_PACKED, false);
+    } else if (entry16) {
+        if (cols) SUPER_L(KEYS_ENTRY, true); else SUPER_L(KEYS_ENTRY, false);
+    } else {
+        if (cols) SUPER_L(KEYS_STRIDED, true); else SUPER_L(KEYS_STRIDED, false);
+    }
+#undef SUPER_L
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess || cols) return e;
+    return launch_runs_transpose(ws, stream);
+}
+
+inline hipError_t launch_bin_super_impl(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                                        hipStream_t stream) {
+    if (ws.nbins > 4095) return hipErrorInvalidValue;
+    SegMap sm{};
+    switch (pass1_plan(mp, ws, false, &sm)) {
+        case kModP2: return launch_bin_super_mk<kModP2>(ks, mp, ws, sm, stream);
+        case kModFast: return launch_bin_super_mk<kModFast>(ks, mp, ws, sm, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 // Pass 1 for a build (SLOTS = false) or a probe (SLOTS = true), then the
 // run-start transpose when the table is large: the exported instantiation
 // for the batch's tile size.
@@ -1467,11 +1795,13 @@ template <bool SLOTS>
 hipError_t launch_bin(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                       uint16_t *slots, hipStream_t stream) {
     const bool big = tile_keys_of(ws) == 2 * kPartTileKeys;
-    if constexpr (SLOTS)
+    if constexpr (SLOTS) {
         return big ? launch_bin_probe1024(ks, mp, ws, slots, stream)
                    : launch_bin_probe512(ks, mp, ws, slots, stream);
-    else
+    } else {
+        if (tile_keys_of(ws) == kSuperTileKeys) return launch_bin_super(ks, mp, ws, stream);
         return big ? launch_bin_build1024(ks, mp, ws, stream) : launch_bin_build512(ks, mp, ws, stream);
+    }
 }
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
@@ -1590,6 +1920,16 @@ hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *w
 template <int MODE>
 hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *words, uint64_t nw32,
                         int merge, uint8_t *res, const StackTable &st, hipStream_t stream) {
+    if constexpr (MODE == kApplyBuild) {
+        if (tile_keys_of(ws) == kSuperTileKeys) {
+            // super-tiles: >= kSuperMinBins segments, runs of at most 48
+            // entries on average: independent groups of 4 lanes
+            constexpr int TK = (int)kSuperTileKeys;
+            if (3 * TK / ws.nbins < 24)
+                return launch_apply_g<MODE, 4, TK, 1, 2>(ws, m, words, nw32, merge, res, st, stream);
+            return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
+        }
+    }
     return tile_keys_of(ws) == 2 * kPartTileKeys
                ? launch_apply_tk<MODE, 2 * (int)kPartTileKeys>(ws, m, words, nw32, merge, res, st,
                                                                stream)

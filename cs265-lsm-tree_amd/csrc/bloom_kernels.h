@@ -123,6 +123,12 @@ inline SegMap seg_map_of(const PartitionWorkspace &ws) {
 inline uint32_t choose_tile_keys(size_t nbins) {
     return nbins > 256 ? 2 * (uint32_t)kPartTileKeys : (uint32_t)kPartTileKeys;
 }
+// Builds on many short runs (segments of m < 2^32, at least kSuperMinBins of
+// them: C4's 2,458) sort super-tiles of two 8192-key halves in pass 1
+// (k_part_bin2): runs twice as long, half the (tile, segment) pairs.
+constexpr size_t kSuperTileKeys = 4 * kPartTileKeys;  // 16384
+constexpr size_t kSuperMinBins = 1024;
+constexpr size_t kSuperMaxBins = 4095;                // the rank fields: bins << 20
 inline size_t tile_keys_of(const PartitionWorkspace &ws) {
     return ws.tile_keys ? ws.tile_keys : kPartTileKeys;
 }

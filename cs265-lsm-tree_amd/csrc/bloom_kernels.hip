@@ -593,6 +593,8 @@ bool plan_segments(uint64_t m, int ncu, PartitionWorkspace *ws) {
 
 bool plan_build(uint64_t m, int ncu, PartitionWorkspace *ws) {
     if (!plan_segments(m, ncu, ws)) return false;
+    if (m <= 0xFFFFFFFFull && ws->nbins >= kSuperMinBins && ws->nbins <= kSuperMaxBins)
+        ws->tile_keys = (uint32_t)kSuperTileKeys;  // many short runs: super-tiles (k_part_bin2)
     uint32_t d = 0, t = 0;
     if (!p2_form(m, &d, &t)) return true;
     uint32_t u = 0;
@@ -607,6 +609,7 @@ bool plan_build(uint64_t m, int ncu, PartitionWorkspace *ws) {
     ws->lad_u = u;
     ws->lad_hb = 0;
     ws->seg_bits = d << sl;  // the bin's image: d blocks of 2^s bits
+    ws->tile_keys = 0;       // the ladder build keeps k_part_bin's tiles
     return true;
 }
 

@@ -381,6 +381,27 @@ extern "C" int ubench_ladder(int variant, int tile_keys, const void *keys, size_
         case 1: e = launch_bin<true>(ks, mp, ws, slots, s); break;
         case 2: e = launch_apply_ladder(ws, ms[0], res, st, s); break;
         case 5: e = launch_combine(ws, res, slots, n, out, nw, st, s); break;
+        case 11: case 12: {
+            // pass 1 of the product's geometry WITHOUT the slot stores (11:
+            // the sorted tile and runs as the product writes them; 12: also
+            // no sorted-tile stores): what the slot plane and the tile's
+            // write-out cost C3's pass 1
+            SegMap sm{};
+            if (pass1_plan(mp, ws, true, &sm) != kModLadder || ws.tile_keys != 8192) return -22;
+            const bool cols = runs_as_columns(ws);
+            uint32_t *rt = cols ? ws.run_starts : ws.run_rows;
+            const unsigned g = (unsigned)std::min<size_t>(ws.ntiles, (size_t)device_cu_count());
+            if (variant == 11) {
+                if (cols) k_part_bin<KEYS_PACKED, false, true, 1024, kModLadder, 1023, 4><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
+                else k_part_bin<KEYS_PACKED, false, false, 1024, kModLadder, 1023, 4><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
+            } else {
+                if (cols) k_part_bin<KEYS_PACKED, false, true, 1024, kModLadder, 1023, 4, true><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
+                else k_part_bin<KEYS_PACKED, false, false, 1024, kModLadder, 1023, 4, true><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
+            }
+            e = hipGetLastError();
+            if (e == hipSuccess && !cols) e = launch_runs_transpose(ws, s);
+            break;
+        }
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

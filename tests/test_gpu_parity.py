@@ -62,6 +62,53 @@ def test_build_matches_oracle(coracle, m, strategy):
     assert (f.words() == coracle.build(m, keys)).all()
 
 
+# ----------------------------------------------- super-tile pass 1 builds ----
+# Builds on >= 1024 segments (m > ~1.07 Gbit, below 2^32) sort super-tiles of
+# 16,384 keys (k_part_bin2: half A stashed in LDS, half B in registers, one
+# joint histogram, two output phases): m = 1.4e9 (general remainder, 1,187
+# segments), C4's 3 << 30 (p2 remainder, 2,458) and 2^32 - 1 (3,277).
+SUPER_MS = [1_400_000_000, 3 * 2**30, 2**32 - 1]
+
+
+@pytest.mark.parametrize("m", SUPER_MS)
+@pytest.mark.parametrize("n", [1, 8191, 8192, 8193, 16_383, 16_385, 40_000, 100_003])
+def test_super_tile_build_matches_oracle(coracle, m, n):
+    """Tiles whose B half is empty, partial or full, a short last super-tile,
+    several tiles: every case bit-exact against the oracle."""
+    keys = rand_keys(n, seed=n % 977 + m % 13)
+    f = bh.BloomFilter(m)
+    f.set_strategy(bh.BUILD_PARTITION)  # AUTO takes atomics below 2^16 keys
+    f.set_batch(keys)
+    assert (f.words() == coracle.build(m, keys)).all()
+
+
+@pytest.mark.parametrize("m", SUPER_MS[:2])
+def test_super_tile_build_layouts_and_skew(coracle, m):
+    """entry_t keys at stride 8 (16-B aligned: the vector key loads), keys at
+    stride 12, and a skewed batch (one key repeated across a whole tile: a
+    run of 49,152 entries, the rank field's maximum) mixed with random keys."""
+    rng = np.random.default_rng(5)
+    keys = rand_keys(70_001, seed=11)
+    aos = np.zeros((keys.size, 3), dtype=np.int32)
+    aos[:, 0] = keys
+    want = coracle.build(m, keys)
+    f = bh.BloomFilter(m)
+    f.set_strategy(bh.BUILD_PARTITION)
+    f.set_batch(np.ascontiguousarray(aos[:, :2]).reshape(-1), n=keys.size, stride=8)
+    assert (f.words() == want).all()
+    g = bh.BloomFilter(m)
+    g.set_strategy(bh.BUILD_PARTITION)
+    g.set_batch(aos.reshape(-1), n=keys.size, stride=12)
+    assert (g.words() == want).all()
+    skew = np.concatenate([np.full(16_384, 12345, dtype=np.int32), keys[:30_000],
+                           np.full(20_000, -7, dtype=np.int32)])
+    rng.shuffle(skew[16_384:])
+    h = bh.BloomFilter(m)
+    h.set_strategy(bh.BUILD_PARTITION)
+    h.set_batch(skew)
+    assert (h.words() == coracle.build(m, skew)).all()
+
+
 @pytest.mark.parametrize("strategy", STRATEGIES, ids=["atomic", "lds", "partition"])
 def test_build_device_keys_and_accumulation(coracle, torch_cuda, strategy):
     torch = torch_cuda

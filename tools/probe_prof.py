@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """C3 probe (16.8M GETs x 5 level filters) repeated under one strategy, for
 rocprofv3 --kernel-trace --stats: `python tools/probe_prof.py [auto|stacked|
-partition|gather|route] [reps]` (route: the C3 GET routing, bloomhip_route_gets,
-over runs built with their fences)."""
+partition|gather|route] [reps] [alt|-] [c3|f10]` (route: the GET routing,
+bloomhip_route_gets, over runs built with their fences; f10: the f = 10
+tree's three levels instead of C3's five)."""
 import os
 import sys
 
@@ -24,7 +25,8 @@ def main():
     st = {"auto": bh.PROBE_AUTO, "route": bh.PROBE_AUTO, "stacked": bh.PROBE_STACKED, "partition": bh.PROBE_PARTITION,
           "gather": bh.PROBE_GATHER}[kind]
     torch.cuda.set_device(0)
-    gets, levels = W.c3()
+    workload = sys.argv[4] if len(sys.argv) > 4 else "c3"
+    gets, levels = W.c3() if workload == "c3" else W.f10()
     dgets = torch.from_numpy(gets).cuda()
     filters = []
     for lvl, keys, m in levels:

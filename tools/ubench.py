@@ -309,6 +309,7 @@ def ladder_ablation(levels_sel=(0, 1, 2, 3, 4), reps=20):
             print(json.dumps({"check": f"ladder tk={tk} pass-2 variant {v} == segment stack",
                               "ok": bool(ok and torch.equal(ref, out))}), flush=True)
     names = {0: "all three", 1: "pass 1 (+slots)", 2: "pass 2 (product)", 5: "combine",
+             11: "pass 1 without the slot stores", 12: "pass 1 without slot and tile stores",
              100: "all three (table planner)", 102: "pass 2 (table planner)"}
     names.update({v: (f"all three, chunks of {v - 200} Mi keys" if v > 200 else f"pass 2 variant {v}")
                   for v in variants if v not in names})
