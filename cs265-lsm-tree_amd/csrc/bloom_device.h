@@ -1008,7 +1008,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     // segment's run, which an XCD neighbour reads next from the same L2
     // (C2 pass 2 35.5 -> 39.5 us with the redirect, profiles/r05/redirect/).
     auto vload = [&](uint32_t vi, uint32_t vb, uint32_t end) -> uint32_t {
-        if constexpr (WALK == 2) return 6 * vi < end ? vi : vb;
+        if constexpr (WALK >= 2) return 6 * vi < end ? vi : vb;
         return vi;
     };
     // The six entries of vector vi of tile t; run = [r.x, r.y).
@@ -1153,7 +1153,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         }
     };
 
-    if constexpr (WALK >= 1) {
+    if constexpr (WALK == 1 || WALK == 2) {
         // Independent lane groups: group q (G lanes) walks tiles q, q + Q,
         // q + 2Q, ... one step (G vectors) per iteration, moving to its next
         // tile as soon as its run ends, so no group waits for the longest run
@@ -1190,6 +1190,40 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             const uint4 v2 = load(min(t2, ntiles - 1), vload(vb2 + sub, vb2, r2 >> 16));
             if (t < ntiles && 6 * vb < (r >> 16)) apply6(v, t, vb + sub, dec(r));
             t = t2; r = r2; rn = rn2; vb = vb2; v = v2;
+        }
+    } else if constexpr (WALK == 3) {
+        // The same walk with two vectors per lane per step (vectors vb + sub
+        // and vb + G + sub: a step covers 12G entries), loads past a run's
+        // end redirected as at WALK 2: runs a little longer than one G-vector
+        // step (super-tiles: ~20 entries, 4-5 vectors) take one step.
+        constexpr int kGroupsPerWave = 64 / G;
+        const int Q = kGroupsPerWave * (BLOCK / 64);
+        auto bnd = [&](int tt) -> uint32_t {
+            return tt < ntiles ? run_starts[(size_t)b * ntiles + rt(tt)] : 0u;
+        };
+        int t = wave * kGroupsPerWave + tl;
+        uint32_t r = bnd(t), rn = bnd(t + Q);
+        uint32_t vb = (r & 0xFFFFu) / 6u;
+        uint4 v = load(min(t, ntiles - 1), vload(vb + sub, vb, r >> 16));
+        uint4 w = load(min(t, ntiles - 1), vload(vb + G + sub, vb, r >> 16));
+        while (__ballot(t < ntiles) != 0) {
+            int t2 = t;
+            uint32_t r2 = r, vb2 = vb + 2 * G;
+            const bool adv = 6 * vb2 >= (r >> 16);
+            if (adv) {
+                t2 += Q;
+                r2 = rn;
+                vb2 = (r2 & 0xFFFFu) / 6u;
+            }
+            uint32_t rn2 = rn;
+            if (adv) rn2 = bnd(t2 + Q);
+            const uint4 v2 = load(min(t2, ntiles - 1), vload(vb2 + sub, vb2, r2 >> 16));
+            const uint4 w2 = load(min(t2, ntiles - 1), vload(vb2 + G + sub, vb2, r2 >> 16));
+            if (t < ntiles && 6 * vb < (r >> 16)) {
+                apply6(v, t, vb + sub, dec(r));
+                apply6(w, t, vb + G + sub, dec(r));
+            }
+            t = t2; r = r2; rn = rn2; vb = vb2; v = v2; w = w2;
         }
     } else {
     uint32_t rp[DEPTH];  // this batch's bounds, packed
@@ -1926,7 +1960,7 @@ hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *word
             // entries on average: independent groups of 4 lanes
             constexpr int TK = (int)kSuperTileKeys;
             if (3 * TK / ws.nbins < 24)
-                return launch_apply_g<MODE, 4, TK, 1, 2>(ws, m, words, nw32, merge, res, st, stream);
+                return launch_apply_g<MODE, 4, TK, 1, 3>(ws, m, words, nw32, merge, res, st, stream);
             return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
         }
     }
