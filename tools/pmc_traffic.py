@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import pmc_summary  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BUILD_KERNELS = ("k_part_bin", "k_runs_transpose", "k_part_apply", "k_build_lds",
+BUILD_KERNELS = ("k_part_bin", "k_part_bin2", "k_runs_transpose", "k_part_apply", "k_build_lds",
                  "k_build_atomic")
 
 
@@ -83,6 +83,7 @@ def per_kernel(d):
 # FETCH_SIZE: every request the L2 sends is one 128-B line, tallied at 64 B).
 KERNEL_SHAPES = {
     "k_part_bin": {"read": [0], "write": [7, 9]},        # keys; sorted tiles + run-table columns
+    "k_part_bin2": {"read": [0], "write": [7, 9]},       # the same on super-tiles
     "k_runs_transpose": {"read": [0], "write": [7]},
     "k_part_apply": {"read": [3, 4, 5, 6], "write": [7, 8]},  # run walks; segments / result bytes
     "k_probe_combine": {"read": [0], "write": [7]},       # slots + result bytes (+ keys when routing)
