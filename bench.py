@@ -253,6 +253,28 @@ def time_leg(call, torch, prewarm_s=LEG_PREWARM_S, calls=LEG_MIN_CALLS, sync=Non
     return (time.perf_counter() - t0) / max(calls, 1), n
 
 
+COMPUTE_CEILING = os.path.join("profiles", "r05", "compute_ceiling.json")
+
+
+def compute_ceiling(case, achieved):
+    """The VALU ceiling of a workload's pass 1 (tools/ubench.py prim: the three
+    hashes plus each position's bin and entry exactly as k_part_bin forms
+    them for this geometry, compute only; profiles/r05/compute_ceiling.json)
+    beside the achieved rate: the build cannot beat its own arithmetic."""
+    path = os.path.join(ROOT, COMPUTE_CEILING)
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    c = d["pass1_arithmetic"].get(case)
+    if not c:
+        return None
+    return {"bound": "valu", "unit": "Gkeys/s", "pass1_arithmetic": c["Gkeys_s"],
+            "reduction": c["reduction"], "achieved": round(achieved, 2),
+            "frac": round(achieved / c["Gkeys_s"], 4),
+            "hash3_mod_p2": d["hash3_mod_p2"].get(str(c["m"][0])),
+            "source": f"{COMPUTE_CEILING} ({case}; from {d['source'].split(' ')[0]})"}
+
+
 def load_pins():
     path = os.path.join(ROOT, "tests", "golden", "pins.json")
     if not os.path.exists(path):
@@ -318,6 +340,9 @@ def probe_leg(torch, bh, workload="c3"):
             "traffic_ratio": round(traffic / algo, 2) if traffic else None,
             "traffic_source": "profiles/pmc_c3.json" if traffic else None,
             "hits_per_level": hit_counts,
+            "compute_ceiling": compute_ceiling("C3 probe (5-level ladder)" if workload == "c3"
+                                               else "f10 probe (3 levels, m = 5.12M * 10^i)",
+                                               gets.size / (kms * 1e-3) / 1e9),
             "hits_sha_match": sha_ok}
 
 
@@ -479,7 +504,8 @@ def compact_fanin(torch, bh):
                     "of the merged run built; wall clock per synchronous call"}
 
 
-def build_leg(torch, bh, keys, m, pin_sha, traffic_workload=None, reps=LEG_MIN_CALLS):
+def build_leg(torch, bh, keys, m, pin_sha, traffic_workload=None, reps=LEG_MIN_CALLS,
+              ceiling_case=None):
     """One device-resident build of `keys` into m bits, repeated: the bitmap
     is checked against the oracle's SHA-256 pin; the device time per build
     comes from HIP events on the launch stream around `reps` back-to-back
@@ -532,6 +558,8 @@ def build_leg(torch, bh, keys, m, pin_sha, traffic_workload=None, reps=LEG_MIN_C
                         "traffic_ratio": round(traffic / algo, 2) if traffic else None,
                         "traffic_source": f"profiles/pmc_{traffic_workload}.json" if traffic else None,
                         "algorithmic_bytes": algo},
+           "compute_ceiling": compute_ceiling(ceiling_case, n / (dev_ms * 1e-3) / 1e9)
+           if ceiling_case else None,
            "verified_vs_oracle": ok}
     del dk, f
     return out
@@ -545,7 +573,7 @@ def c4_build(torch, bh, reps=LEG_MIN_CALLS):
     keys, m = W.c4()
     pins = load_pins()
     out = build_leg(torch, bh, keys, m, pins["oracle"]["c4"]["sha256"] if pins else None,
-                    traffic_workload="c4", reps=reps)
+                    traffic_workload="c4", reps=reps, ceiling_case="C4 build")
     bh.lib().bloomhip_trim()  # the 3 GB partition workspace of this size
     torch.cuda.empty_cache()
     return out
@@ -562,7 +590,8 @@ def f10_legs(torch, bh):
     keys, m = W.f10_build()
     pins = load_pins()
     pin = pins["oracle"].get("f10") if pins else None
-    return {"build": build_leg(torch, bh, keys, m, pin["build"]["sha256"] if pin else None),
+    return {"build": build_leg(torch, bh, keys, m, pin["build"]["sha256"] if pin else None,
+                               ceiling_case="f10 build (b=1000, f=10, r=10: m = 15625 << 15)"),
             "probe": probe_leg(torch, bh, "f10"),
             "note": "reference's published tree b=1000 f=10 at 10 bits/entry: "
                     "m_i = 5,120,000*10^i (odd part 625*5^i)"}
@@ -937,13 +966,13 @@ def main():
                      "note": "achieved = (4N + m/8) per build / device time per build, HIP "
                              "events on the launch stream around the unprofiled timed loop; "
                              "profiled_kernel_ms = per-launch events in a separate pass"},
-        # The build's real ceiling is the VALU: the reference's three 64-bit hashes and
-        # exact remainders alone run at 437-446 Gkeys/s on this chip (tools/ubench.py,
-        # compute only), i.e. 2.3 TB/s = 0.29 of HBM at 5.25 B/key.
-        "compute_ceiling": {"bound": "valu", "unit": "Gkeys/s", "hash_mod_only": 437.0,
-                            "achieved": round(n / (dev_ms_per_step * 1e-3) / 1e9, 2),
-                            "frac": round(n / (dev_ms_per_step * 1e-3) / 1e9 / 437.0, 4),
-                            "source": "profiles/r02/s3/evidence/ub_prim.log (hash3+mod_fast, m = C2)"},
+        # The build's real ceiling is the VALU: pass 1's own arithmetic (the reference's
+        # three 64-bit hashes, the p2 remainder and the bin/entry of each position as
+        # k_part_bin forms them) runs at ~531 Gkeys/s on this chip for C2 (compute only,
+        # DESIGN.md §4), i.e. 2.8 TB/s = 0.35 of HBM at 5.25 B/key.
+        "compute_ceiling": compute_ceiling({"c2": "C2 build", "c5": "C5 build",
+                                            "c4": "C4 build"}.get(args.workload, ""),
+                                           n / (dev_ms_per_step * 1e-3) / 1e9),
         "clocks": clocks,
         "library": {"kernel_sha": library_kernel_sha(),
                     "matches_sources": library_kernel_sha() == kernel_source_sha()},
