@@ -231,11 +231,15 @@ extern "C" int ubench_pass1_arith(int nf, const uint64_t *ms, int grid, int bloc
 // (tools/ubench.py sizes its buffers from it): segments, segment bits, tile
 // keys and tiles.
 // out4: segments, segment bits, tile keys, tiles.
+// out4: the larger of plan_build's and plan_segments' segment counts, the
+// product's segment bits, the smallest tile of the two plans and the tiles
+// at that size: buffers sized from these hold every variant of ubench_part.
 extern "C" int ubench_part_geometry(size_t n, uint64_t m, uint64_t *out4) {
-    PartitionWorkspace ws{};
-    if (!plan_segments(m, device_cu_count(), &ws)) return -34;
-    const size_t tk = choose_tile_keys(ws.nbins);
-    out4[0] = ws.nbins;
+    PartitionWorkspace ws{}, sg{};
+    if (!plan_build(m, device_cu_count(), &ws) || !plan_segments(m, device_cu_count(), &sg)) return -34;
+    const size_t tk = std::min<size_t>(ws.tile_keys ? ws.tile_keys : choose_tile_keys(ws.nbins),
+                                       choose_tile_keys(sg.nbins));
+    out4[0] = std::max(ws.nbins, sg.nbins);
     out4[1] = ws.seg_bits;
     out4[2] = tk;
     out4[3] = (n + tk - 1) / tk;
@@ -247,7 +251,8 @@ extern "C" int ubench_part_geometry(size_t n, uint64_t m, uint64_t *out4) {
 // it over variant 0's output; 5001 / 5003 = pass-1 shapes (MINW waves per
 // SIMD, NWG workgroups per CU).  runs: both table layouts.
 extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, uint64_t *pos,
-                           uint32_t *runs, uint32_t *words, void *stream) {
+                           uint32_t *runs, uint32_t *words, void *stream, size_t pos_cap,
+                           size_t runs_cap) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const KeySpan ks{reinterpret_cast<const char *>(keys), n, 4, KEYS_PACKED};
     const ModParams mp = make_mod_params(m);
@@ -257,8 +262,11 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     const bool seg = variant == 20 || variant == 21;
     if (!(seg ? plan_segments(m, device_cu_count(), &ws) : plan_build(m, device_cu_count(), &ws)))
         return -34;
-    ws.tile_keys = choose_tile_keys(ws.nbins);
+    if (!ws.tile_keys) ws.tile_keys = choose_tile_keys(ws.nbins);  // plan_build's super-tiles kept
     ws.ntiles = (n + ws.tile_keys - 1) / ws.tile_keys;
+    // the caller's buffers must hold this plan's tiles (pos, in u64) and
+    // both run-table layouts (runs, in u32): refused, not overrun
+    if (ws.ntiles * ws.tile_keys > pos_cap || 2 * ws.ntiles * (ws.nbins + 1) > runs_cap) return -28;
     ws.pos = pos;
     ws.run_rows = runs;
     ws.run_starts = runs + ws.ntiles * (ws.nbins + 1);

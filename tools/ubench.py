@@ -19,7 +19,8 @@ LIB.ubench_run.restype = ctypes.c_int
 LIB.ubench_part_geometry.argtypes = [ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p]
 LIB.ubench_part_geometry.restype = ctypes.c_int
 LIB.ubench_part.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
-                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_size_t, ctypes.c_size_t]
 LIB.ubench_part.restype = ctypes.c_int
 LIB.ubench_stack.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                              ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_void_p] * 6
@@ -73,7 +74,7 @@ def _part_setup(n, bpe):
 
     def run(v):
         return LIB.ubench_part(v, keys.data_ptr(), n, m, pos.data_ptr(), runs.data_ptr(),
-                               words.data_ptr(), s.cuda_stream)
+                               words.data_ptr(), s.cuda_stream, pos.numel(), runs.numel())
     return run, words, {"n": n, "m": m, "nbins": nbins, "seg_bits": seg_bits, "tile_keys": tk}
 
 
