@@ -1030,14 +1030,20 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             const int s0 = (int)(6 * vi) - (int)r.x;          // entry 0's place in the run
             const int lo = max(-s0, 0), hi = min(max((int)r.y - (int)(6 * vi), 0), 6);
             const uint32_t vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+            // WALK 3 (super-tiles): a lane whose vector holds none of the
+            // run's entries (a redirected load past the run's end: about half
+            // of them at C4's ~20-entry runs) issues no atomics, so the
+            // segment image's banks serve only the lanes with bits to set
+            if (WALK < 3 || vm != 0) {
 #pragma unroll
-            for (int k = 0; k < 6; k++) {
-                const uint32_t d = MODE == kApplyBuildL ? e[k] : e[k] - base21;
-                const uint32_t addr = (d >> 3) & ((kEntryMask >> 3) & ~3u);
-                const uint32_t bit = __builtin_amdgcn_ubfe(vm, k, 1) << (d & 31);
-                __attribute__((address_space(3))) uint32_t *w =
-                    (__attribute__((address_space(3))) uint32_t *)(size_t)addr;
-                __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int k = 0; k < 6; k++) {
+                    const uint32_t d = MODE == kApplyBuildL ? e[k] : e[k] - base21;
+                    const uint32_t addr = (d >> 3) & ((kEntryMask >> 3) & ~3u);
+                    const uint32_t bit = __builtin_amdgcn_ubfe(vm, k, 1) << (d & 31);
+                    __attribute__((address_space(3))) uint32_t *w =
+                        (__attribute__((address_space(3))) uint32_t *)(size_t)addr;
+                    __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             }
         } else {
             uint32_t bits[6], mask = 0;
