@@ -1034,7 +1034,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             // run's entries (a redirected load past the run's end: about half
             // of them at C4's ~20-entry runs) issues no atomics, so the
             // segment image's banks serve only the lanes with bits to set
-            if (WALK < 3 || vm != 0) {
+            if (WALK < 1 || vm != 0) {
 #pragma unroll
                 for (int k = 0; k < 6; k++) {
                     const uint32_t d = MODE == kApplyBuildL ? e[k] : e[k] - base21;
