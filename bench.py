@@ -350,12 +350,13 @@ def probe_c3(torch, bh):
     return probe_leg(torch, bh, "c3")
 
 
-def route_c3(torch, bh):
+def route_c3(torch, bh, workload="c3"):
     """§8f row 1: batched GET routing of C3's 16.8M GETs over the five level
     runs (range check + filter probe + newest candidate + page index), all
-    outputs device-resident."""
+    outputs device-resident; workload "f10": the same GETs over the f = 10
+    tree's three level runs (13,875 fences)."""
     from bloomhip import workloads as W
-    gets, levels = W.c3_runs()
+    gets, levels = W.c3_runs() if workload == "c3" else W.f10_runs()
     runs = []
     for lvl, keys, m in levels:
         f = bh.BloomFilter(m)
@@ -593,6 +594,7 @@ def f10_legs(torch, bh):
     return {"build": build_leg(torch, bh, keys, m, pin["build"]["sha256"] if pin else None,
                                ceiling_case="f10 build (b=1000, f=10, r=10: m = 15625 << 15)"),
             "probe": probe_leg(torch, bh, "f10"),
+            "route": route_c3(torch, bh, "f10"),
             "note": "reference's published tree b=1000 f=10 at 10 bits/entry: "
                     "m_i = 5,120,000*10^i (odd part 625*5^i)"}
 

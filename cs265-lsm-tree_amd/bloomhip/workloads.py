@@ -148,3 +148,10 @@ def f10(seed: int = SEED):
         start += cap
     levels.sort(key=lambda t: t[0])
     return gets, levels
+
+
+def f10_runs(seed: int = SEED):
+    """f10() with each level's run as the reference writes it (distinct keys
+    ascending, as c3_runs): the same filters, plus fences for GET routing."""
+    gets, levels = f10(seed)
+    return gets, [(lvl, np.unique(keys), m) for lvl, keys, m in levels]

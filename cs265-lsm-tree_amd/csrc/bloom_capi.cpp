@@ -831,7 +831,7 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
         // every filter of a routing call in this one stack: the routing runs
         // in its combine (k_probe_combine_route), not in k_route afterwards
         const bool fuse = route && (int)mem.size() == nf && route->rt->nruns == nf &&
-                          (size_t)route->rt->total_fences * 4 <= kRouteLdsFenceBytes;
+                          (size_t)route->rt->total_fences * 4 <= kRouteLdsFenceBytesMax;
         hipError_t e = timed(f0, fuse ? SLOT_PROBE_STACK_ROUTE : SLOT_PROBE_STACK, s, [&] {
             return fuse ? launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s,
                                                route->rt, route->first, route->page)

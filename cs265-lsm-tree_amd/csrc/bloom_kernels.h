@@ -36,7 +36,12 @@ struct ProbeTable {
 // Run metadata and GET routing (§8f rows 1, 4).
 constexpr size_t kFenceStride = 4096;  // getpagesize() entries per fence, src/run.cpp:164
 constexpr int kMaxRouteRuns = 64;
-constexpr size_t kRouteLdsFenceBytes = 48u << 10;  // fences of all runs staged in LDS up to this
+// Routing stages every run's fences in LDS up to this (k_route, and the
+// combine with routing fused in, which runs one workgroup per CU instead of
+// two above ~56 KB): the f = 10 tree's three runs have 13,875 fences, 55 KB,
+// and a binary search in global memory took 0.59 ms for its 16.8M GETs.
+// Dynamic LDS within 64 KiB needs no opt-in.
+constexpr size_t kRouteLdsFenceBytesMax = 60u << 10;
 
 // Run metadata on the device: meta[0] = max key, meta[1 .. nfences] = the
 // fence pointers, ascending (a run is written sorted).
@@ -289,7 +294,7 @@ hipError_t launch_route(const KeySpan &keys, const RouteTable &t, uint64_t *cand
 // probe.  Row st.row[j] of out (nw words per row) gets member j's results.
 // rt (GET routing fused into the combine, k_probe_combine_route): every run
 // of the routing call is a member (rt->nruns == st.nf, st.row a permutation)
-// and their fences fit kRouteLdsFenceBytes; out then gets the range-checked
+// and their fences fit kRouteLdsFenceBytesMax; out then gets the range-checked
 // candidate rows and first / page (either may be null) what k_route writes.
 hipError_t launch_probe_stacked(const KeySpan &keys, const ModParams &mp_max, const StackTable &st,
                                 const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,

@@ -871,7 +871,7 @@ hipError_t launch_route(const KeySpan &ks, const RouteTable &t, uint64_t *cand, 
     // Fences from LDS beat L2 reads.  The grid is what fits on the chip at
     // once (the staged fences bound the workgroups per CU), and every wave
     // walks many 64-key steps, so each workgroup stages the fences once.
-    const bool in_lds = lds <= kRouteLdsFenceBytes;
+    const bool in_lds = lds <= kRouteLdsFenceBytesMax;
     const size_t per_block = (in_lds ? lds : 0) + 2048;
     int per_cu = (int)(kLdsBitmapBytes / per_block);
     per_cu = per_cu < 1 ? 1 : per_cu > 8 ? 8 : per_cu;  // 8 x 256 threads = 32 waves per CU

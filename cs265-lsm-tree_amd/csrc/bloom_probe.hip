@@ -46,7 +46,7 @@ hipError_t launch_combine_route(const PartitionWorkspace &ws, const uint8_t *res
                                 const uint16_t *slots, const KeySpan &ks, uint64_t *out, size_t nw,
                                 const StackTable &rows, const RouteTable &rt, int32_t *first,
                                 int32_t *page, hipStream_t stream) {
-    if (rt.nruns != rows.nf || (size_t)rt.total_fences * 4 > kRouteLdsFenceBytes) return hipErrorInvalidValue;
+    if (rt.nruns != rows.nf || (size_t)rt.total_fences * 4 > kRouteLdsFenceBytesMax) return hipErrorInvalidValue;
     unsigned seen = 0;
     for (int j = 0; j < rows.nf; j++) {
         if (rows.row[j] < 0 || rows.row[j] >= rows.nf) return hipErrorInvalidValue;
@@ -55,7 +55,12 @@ hipError_t launch_combine_route(const PartitionWorkspace &ws, const uint8_t *res
     if (seen != (1u << rows.nf) - 1u) return hipErrorInvalidValue;
     constexpr int kBig = 2 * (int)kPartTileKeys, kSmall = (int)kPartTileKeys;
     const size_t lds = (size_t)rt.total_fences * 4;
-    const size_t cap = (size_t)device_cu_count() * 2;  // two 1024-thread workgroups per CU
+    // persistent workgroups, as many as are resident at once: two per CU
+    // while two copies of the fences and the tile's result bytes fit the
+    // LDS, else one (a second round of workgroups would start only when the
+    // first has walked all of its tiles)
+    const size_t per_wg = lds + 3 * (size_t)kBig + 1024;
+    const size_t cap = (size_t)device_cu_count() * (2 * per_wg <= kLdsBitmapBytes ? 2 : 1);
     const unsigned grid = (unsigned)(ws.ntiles < cap ? ws.ntiles : cap);
 #define COMBINE_ROUTE(TK, L)                                                                      \
     k_probe_combine_route<TK, TK / kCombineKeys, L><<<grid, TK / kCombineKeys, lds, stream>>>(    \
@@ -75,7 +80,7 @@ hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, cons
                                 uint64_t *out, size_t nw, hipStream_t stream, const RouteTable *rt,
                                 int32_t *first, int32_t *page) {
     if (ks.n == 0) return hipSuccess;
-    if (rt && (rt->nruns != st.nf || (size_t)rt->total_fences * 4 > kRouteLdsFenceBytes))
+    if (rt && (rt->nruns != st.nf || (size_t)rt->total_fences * 4 > kRouteLdsFenceBytesMax))
         return hipErrorInvalidValue;
     auto combine = [&]() {
         return rt ? launch_combine_route(ws, res, slots, ks, out, nw, st, *rt, first, page, stream)

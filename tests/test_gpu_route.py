@@ -4,6 +4,8 @@ built beside the filter, and batched GET routing (range check + filter probe
 Run::put / Run::get / LSMTree::get (oracle/bloom_oracle.c bo_run_meta,
 bo_route).  Bit-exact: same fences and max key, same candidate rows, same
 first-run and page per key."""
+import hashlib
+
 import numpy as np
 import pytest
 
@@ -210,6 +212,31 @@ def test_route_c3_full(coracle, golden):
     # filter bits are the pinned C3 probe results restricted by the range check
     probe = bh.test_batch(runs, gets)
     assert ((cand & ~probe) == 0).all()
+
+
+def test_route_f10_full(coracle, golden):
+    """The reference's published tree (b = 1000, f = 10: runs of 512,000 *
+    10^i keys): 16.8M GETs over its three level runs, whose 13,875 fences
+    (55 KB) are staged in LDS by the combine with routing fused in at one
+    workgroup per CU; against the oracle, and the path asserted."""
+    from bloomhip import workloads as W
+    gets, levels = W.f10_runs()
+    runs, orefs = [], []
+    for lvl, keys, m in levels:
+        f = bh.BloomFilter(m)
+        f.set_batch_run(keys)
+        runs.append(f)
+        fences, mk = coracle.run_meta(keys)
+        orefs.append((coracle.build(m, keys), m, fences, mk))
+    assert sum(o[2].size for o in orefs) * 4 > 48 << 10  # beyond the round-4 fence budget
+    path, (cand, first, page) = routed_by(runs, lambda: bh.route_gets(runs, gets))
+    assert path == "fused"
+    wc, wf, wp = coracle.route(orefs, gets)
+    assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
+    probe = bh.test_batch(runs, gets)
+    for lvl in range(len(levels)):
+        assert hashlib.sha256(probe[lvl].tobytes()).hexdigest() == \
+            golden["oracle"]["f10"]["levels"][lvl]["hits_sha256"]
 
 
 @pytest.mark.parametrize("layout", ["packed", "entry", "device"])
