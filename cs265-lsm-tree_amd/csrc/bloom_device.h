@@ -517,11 +517,13 @@ __global__ void __launch_bounds__(kSuperBlock, 4) k_part_bin2(KeySpan ks, ModPar
                   "rank fields (the bin nbins, never incremented, included)");
     static_assert(kSuperTileKeys == (size_t)kTileKeys, "super-tile size");
     static_assert(MAXB + 1 + TB / 64 <= kPhasePos, "histogram and wave sums inside the image");
-    // [stash: kStashWords][image: kPhasePos], histogram + wave sums at the
-    // image's start until the phases
-    __shared__ __attribute__((aligned(16))) uint32_t s_pool[kStashWords + kPhasePos];
-    uint2 *stash = reinterpret_cast<uint2 *>(s_pool);
-    uint32_t *img = s_pool + kStashWords;
+    // [image: kPhasePos][stash: kStashWords], histogram + wave sums at the
+    // image's start until the phases.  The image first: an entry's slot is
+    // then its LDS byte address (no add per write), and the stash is reached
+    // through the offset field
+    __shared__ __attribute__((aligned(16))) uint32_t s_pool[kPhasePos + kStashWords];
+    uint32_t *img = s_pool;
+    uint2 *stash = reinterpret_cast<uint2 *>(s_pool + kPhasePos);
     uint32_t *s_hist = img;
     uint32_t *s_wsum = img + MAXB + 1;
     char *img_b = reinterpret_cast<char *>(img);

@@ -107,6 +107,10 @@ def test_super_tile_build_layouts_and_skew(coracle, m):
     h.set_strategy(bh.BUILD_PARTITION)
     h.set_batch(skew)
     assert (h.words() == coracle.build(m, skew)).all()
+    # a second batch into the same filter: pass 2 ORs into the existing bitmap
+    more = rand_keys(33_333, seed=12)
+    h.set_batch(more)
+    assert (h.words() == coracle.build(m, np.concatenate([skew, more]))).all()
 
 
 @pytest.mark.parametrize("strategy", STRATEGIES, ids=["atomic", "lds", "partition"])
