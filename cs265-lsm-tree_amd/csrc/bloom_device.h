@@ -12,6 +12,9 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+#include <numeric>
+
 #include "bloom_kernels.h"
 
 namespace bloomhip {
@@ -800,7 +803,22 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     // of the run-start rows, so give consecutive segments to workgroups on one
     // XCD (blocks are dealt round-robin over the 8 XCDs): a bijection on
     // [0, nbins); placement only affects speed.
-    const int b = (int)xcd_remap(blockIdx.x, (unsigned)nbins);
+    // One segment b per workgroup, or (the stacked probe with a segment
+    // stride S, StackTable::seg_stride; a compile-time 0 for every other
+    // mode) segments c, c + S, c + 2S, ...: members whose windows repeat with
+    // a period dividing S (StackTable::keep_mask) are staged for the first
+    // of them only.  Only at G = 4 (short runs, many segments) and up to 7
+    // compiled-in members: the loop took 64 -> 68 VGPRs at 8 members and
+    // 62 -> 65 at G = 8 with 5, which leaves one 1024-lane workgroup per CU.
+    constexpr bool kStrided = MODE == kApplyStack && NF < 8 && G == 4;
+    const int seg_stride = kStrided ? st.seg_stride : 0;
+    uint32_t stage_mask = ~0u;
+    for (int b = (int)xcd_remap(blockIdx.x, seg_stride ? (unsigned)seg_stride : (unsigned)nbins);;) {
+    {
+    // the thread index laundered per segment in the strided loop, which
+    // otherwise hoists thread-dependent addresses out of it (52 -> 61 VGPRs)
+    uint32_t tix = threadIdx.x;
+    if constexpr (kStrided) asm volatile("" : "+v"(tix));
     const uint64_t w0 = (uint64_t)b * seg_words;
     const int nseg = (int)(min(nw32, w0 + seg_words) - w0);  // last segment may be short
     const uint64_t base = (uint64_t)b * seg_bits;
@@ -814,10 +832,11 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         // reaches all of them.
         const int nf = NF ? NF : st.nf;  // NF: the member count as a compile-time constant
         for (int j = 0; j < nf; j++) {
+            if (!((stage_mask >> j) & 1u)) continue;  // its window is already in LDS
             const uint32_t mw = st.mwords[j];
             const uint32_t start = (uint32_t)(((uint64_t)b * seg_words) % mw);
             const uint4 *src = reinterpret_cast<const uint4 *>(st.words[j]);
-            for (int i = threadIdx.x; i < (int)seg_words / 4; i += BLOCK) {
+            for (int i = tix; i < (int)seg_words / 4; i += BLOCK) {
                 uint32_t wi = start + 4u * (uint32_t)i;
                 if (wi >= mw) wi -= mw;
                 const uint4 v = src[wi / 4];
@@ -866,7 +885,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             for (uint32_t j = 0; j < K; j++) {
                 const uint4 *src = reinterpret_cast<const uint4 *>(st.words[j]);
                 uint4 *dst = reinterpret_cast<uint4 *>(seg) + ((size_t)L.base[j] << bv);
-                for (uint32_t q = threadIdx.x; q < (L.nblk[j] << bv); q += BLOCK)
+                for (uint32_t q = tix; q < (L.nblk[j] << bv); q += BLOCK)
                     dst[q] = src[(first_bit(j, q >> bv) >> 7) + (q & ((1u << bv) - 1u))];
             }
         };
@@ -877,7 +896,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         // are staged after the packed image is built from it
         uint32_t *tmap = CT ? seg : tbl + L.ne * L.rs;
         constexpr uint32_t kTupleShift = BPP == 4 ? 0u : 1u;  // tuple words = 2^(s-3+this)
-        for (uint32_t e = CT ? L.ne : threadIdx.x; e < L.ne; e += BLOCK) {
+        for (uint32_t e = CT ? L.ne : tix; e < L.ne; e += BLOCK) {
             const uint32_t amax = e >> L.hb;
             const uint32_t xs = ((e & ((1u << L.hb) - 1u)) << L.u) | bin;  // hash bits [s, t_max)
             for (uint32_t j = 1; j < (uint32_t)NF && j <= K; j++) {
@@ -892,7 +911,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         }
         if constexpr (K < (uint32_t)NF) {
             const uint32_t tk = L.t[K < (uint32_t)kMaxStack ? K : 0], ntup = L.nblk[K];
-            for (uint32_t tp = threadIdx.x; tp < ntup; tp += BLOCK) {
+            for (uint32_t tp = tix; tp < ntup; tp += BLOCK) {
                 // tuple tp = member K's block: a_K and hash bits [s, t_K)
                 uint32_t ak, xs;
                 if (tk >= L.s + L.u) {
@@ -916,7 +935,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             const uint32_t cps = 1u << (L.s - 5);  // 32-position chunks per tuple
             const uint32_t ntask = L.nblk[K] * cps;
             uint32_t *pk = seg + L.pk_words;
-            for (uint32_t q = threadIdx.x; q < ntask; q += BLOCK) {
+            for (uint32_t q = tix; q < ntask; q += BLOCK) {
                 const uint32_t tp = q >> (L.s - 5), c = q & (cps - 1u);
                 uint32_t w[NF];
 #pragma unroll
@@ -960,16 +979,16 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             stage_direct();
         }
     } else if constexpr (MODE == kApplyProbe) {
-        for (int i = threadIdx.x; i < (int)seg_words; i += BLOCK)
+        for (int i = tix; i < (int)seg_words; i += BLOCK)
             seg[i] = i < nseg ? words[w0 + i] : 0u;
     } else {
-        for (int i = threadIdx.x; i < (int)seg_words / 4; i += BLOCK)
+        for (int i = tix; i < (int)seg_words / 4; i += BLOCK)
             reinterpret_cast<uint4 *>(seg)[i] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
 
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int lane = tix & 63;
+    const int wave = tix >> 6;
     const uint32_t sub = (uint32_t)(lane % G);  // this lane's vector in its tile's step
     const int tl = lane / G;                    // this lane's tile in a load group
     const int nbatch = (ntiles + kBatchTiles - 1) / kBatchTiles;
@@ -1262,7 +1281,10 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         for (int d = 0; d < DEPTH; d++) rp[d] = rn[d];
     }
     }
-    if constexpr (PROBE) return;
+    if constexpr (PROBE) {
+        if constexpr (kStrided) goto segment_done;
+        return;
+    }
     __syncthreads();
 
     if constexpr (MODE == kApplyBuildL) {
@@ -1271,7 +1293,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         const uint32_t vpb = 1u << (ls - 7);  // 16-B vectors per block
         const uint4 *seg4 = reinterpret_cast<const uint4 *>(seg);
         uint4 *w4 = reinterpret_cast<uint4 *>(words);
-        for (uint32_t q = threadIdx.x; q < st.lad.d * vpb; q += BLOCK) {
+        for (uint32_t q = tix; q < st.lad.d * vpb; q += BLOCK) {
             const uint32_t a = q >> (ls - 7), i = q & (vpb - 1u);
             uint4 *dq = w4 + (((size_t)a << (lt - 7)) + ((size_t)b << (ls - 7)) + i);
             uint4 v = seg4[q];
@@ -1288,7 +1310,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     if (nseg == (int)seg_words) {  // seg_words % 4 == 0 and w0 is 16-B aligned
         uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
         const uint4 *seg4 = reinterpret_cast<const uint4 *>(seg);
-        for (int q = threadIdx.x; q < (int)seg_words / 4; q += BLOCK) {
+        for (int q = tix; q < (int)seg_words / 4; q += BLOCK) {
             uint4 v = seg4[q];
             if (merge_existing) {
                 const uint4 o = dst4[q];
@@ -1297,11 +1319,19 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             dst4[q] = v;
         }
     } else {
-        for (int i = threadIdx.x; i < nseg; i += BLOCK) {
+        for (int i = tix; i < nseg; i += BLOCK) {
             uint32_t v = seg[i];
             if (merge_existing) v |= dst[i];
             dst[i] = v;
         }
+    }
+    }
+    segment_done:
+        if (!seg_stride) return;
+        b += seg_stride;
+        if (b >= nbins) return;
+        stage_mask = ~st.keep_mask;
+        __syncthreads();  // the walk's last image reads, before the next staging
     }
 }
 
@@ -1848,6 +1878,45 @@ hipError_t launch_bin(const KeySpan &ks, const ModParams &mp, const PartitionWor
 
 // Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
 // must be opted into per kernel).
+// The segment stack's pass 2 on persistent workgroups (round 5): member j's
+// window of segment b starts at word (b * sw) mod mw_j, periodic in b with
+// period P_j = mw_j / gcd(sw, mw_j) (the f = 10 tree at w = 409,600 bits:
+// 25 for level 0, 125 for level 1, every segment for level 2).  With S
+// resident workgroups, S a multiple of the periods of a set of members,
+// workgroup c takes segments c, c + S, c + 2S, ... and stages those members'
+// windows once (the f = 10 tree: 150 KiB staged per segment -> 50 KiB for
+// four of a workgroup's five).  Sets st.seg_stride = 0 when no member
+// repeats within the resident workgroups or each segment has its own anyway.
+inline void stack_stride(size_t nbins, uint32_t seg_words, size_t lds, StackTable &st) {
+    st.seg_stride = 0;
+    st.keep_mask = 0;
+    const size_t per_cu = std::max<size_t>(1, std::min<size_t>(2048 / kApplyBlock, kLdsBitmapBytes / std::max<size_t>(lds, 1)));
+    const uint64_t cap = (uint64_t)device_cu_count() * per_cu;
+    if (nbins <= cap || st.nf < 1 || st.nf > kMaxStack) return;
+    uint64_t P[kMaxStack];
+    int ord[kMaxStack];
+    for (int j = 0; j < st.nf; j++) {
+        P[j] = st.mwords[j] / std::gcd<uint64_t>(seg_words, st.mwords[j]);
+        ord[j] = j;
+    }
+    std::sort(ord, ord + st.nf, [&](int a, int c) { return P[a] < P[c]; });
+    uint64_t L = 1;
+    uint32_t mask = 0;
+    for (int q = 0; q < st.nf; q++) {
+        const int j = ord[q];
+        if (P[j] >= nbins) continue;  // no repeat among the segments
+        const uint64_t l2 = std::lcm<uint64_t>(L, P[j]);
+        if (l2 > cap) continue;
+        L = l2;
+        mask |= 1u << j;
+    }
+    if (!mask) return;
+    const uint64_t S = L * (cap / L);
+    if (S >= nbins) return;
+    st.seg_stride = (int)S;
+    st.keep_mask = mask;
+}
+
 template <int MODE, int G, int TK, int DEPTH = kApplyDepth, int WALK = 0, int NF = 0, int LK = 0>
 hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                           uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
@@ -1869,9 +1938,14 @@ hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *wo
     const size_t lds = MODE == kApplyLadder ? ladder_lds_bytes(st.lad)
                                             : (size_t)ws.seg_bits / 8 * (MODE == kApplyStack ? st.nf : 1);
     if (lds > kStackMaxBits / 8) return hipErrorInvalidValue;
-    k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK, NF, LK><<<(unsigned)ws.nbins, kApplyBlock, lds, stream>>>(
+    StackTable sk = st;
+    sk.seg_stride = 0;
+    sk.keep_mask = 0;
+    if (MODE == kApplyStack && NF < 8 && G == 4) stack_stride(ws.nbins, ws.seg_bits / 32, lds, sk);
+    const unsigned grid = sk.seg_stride ? (unsigned)sk.seg_stride : (unsigned)ws.nbins;
+    k_part_apply<MODE, G, TK, kApplyBlock, DEPTH, WALK, NF, LK><<<grid, kApplyBlock, lds, stream>>>(
         ws.pos, ws.run_starts, (int)ws.ntiles, (int)ws.nbins, ws.seg_bits, m, words, nw32, merge,
-        res, st);
+        res, sk);
     return hipGetLastError();
 }
 

@@ -238,6 +238,11 @@ struct StackTable {
     int nf;
     int ladder;                        // 1: lad holds a ladder geometry (plan_ladder)
     LadderTable lad;
+    // Segment-stack pass 2 only, set at its launch (stack_stride): 0, or the
+    // stride S of the persistent workgroups' segments (b, b + S, ...), and
+    // the members whose windows are the same for all of them (bit j).
+    int seg_stride;
+    uint32_t keep_mask;
 };
 
 // Ladder geometry for members m[0] >= m[1] >= ... (all d << t_j with one d):

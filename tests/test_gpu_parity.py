@@ -339,7 +339,8 @@ def _stack_case(coracle, ms, probe_keys, strategies=None, stride=4, seed=0):
     [5_120_000 * 10**i for i in range(3)],        # the f = 10 tree: gcd 625 << 13 (w = 320,000)
     [256_000 * 10**i for i in range(4)],          # f = 10 at the default r = 0.5: 125 << 11
     [3**7 * 2**9 * 7**i for i in range(3)],       # odd parts 2187 * 7^i, fanout 7
-], ids=["c3x64", "c3_l0-3", "pow2", "no_w", "nine", "mixed", "f10", "f10_r05", "fan7"])
+    [256_000 * 10**i for i in range(1, 4)],       # 625 segments on 250 strided workgroups (2-3 each)
+], ids=["c3x64", "c3_l0-3", "pow2", "no_w", "nine", "mixed", "f10", "f10_r05", "fan7", "r05_l1-3"])
 def test_stacked_probe_matches_oracle(coracle, ms):
     probe = rand_keys(300_001, 77)
     _stack_case(coracle, ms, probe)
