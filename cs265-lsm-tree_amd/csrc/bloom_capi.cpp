@@ -823,15 +823,22 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
             st.mwords[k] = (uint32_t)(filters[mem[k]]->m / 32);
             st.row[k] = mem[k];
         }
+        // every filter of a routing call in this one stack: the routing runs
+        // in its combine (k_probe_combine_route), not in k_route afterwards
+        const bool fuse = route && (int)mem.size() == nf && route->rt->nruns == nf &&
+                          (size_t)route->rt->total_fences * 4 <= kRouteLdsFenceBytesMax;
+        // The fused combine on super-tiles stages 48 KiB of result bytes per
+        // tile: when that and the fences leave one workgroup per CU, 8192-key
+        // tiles (two per CU) route faster (the f = 10 tree: 0.351 against
+        // 0.387 ms, while its plain probe gains from super-tiles)
+        if (fuse && ws.tile_keys == kSuperTileKeys &&
+            2 * ((size_t)route->rt->total_fences * 4 + 3 * kSuperTileKeys + 1024) > kLdsBitmapBytes)
+            ws.tile_keys = 0;
         const LockedWorkspace w(f0->device, s);
         int rc = partition_buffers(w.get(), n, s, &ws);
         if (rc) return rc;
         rc = probe_buffers(w.get(), ws, s);
         if (rc) return rc;
-        // every filter of a routing call in this one stack: the routing runs
-        // in its combine (k_probe_combine_route), not in k_route afterwards
-        const bool fuse = route && (int)mem.size() == nf && route->rt->nruns == nf &&
-                          (size_t)route->rt->total_fences * 4 <= kRouteLdsFenceBytesMax;
         hipError_t e = timed(f0, fuse ? SLOT_PROBE_STACK_ROUTE : SLOT_PROBE_STACK, s, [&] {
             return fuse ? launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s,
                                                route->rt, route->first, route->page)

@@ -501,11 +501,14 @@ __device__ __forceinline__ void load_half_keys(const KeySpan &ks, size_t tile, i
     }
 }
 
-template <int LAYOUT, bool COLS, int MK, int MAXB>
+// SLOTS (the stacked probe's pass 1 on super-tiles): also each key's sorted
+// index per hash, u16 (< 49,152), in the slot plane [tile][hash][key] the
+// combine reads.
+template <int LAYOUT, bool COLS, int MK, int MAXB, bool SLOTS = false>
 __global__ void __launch_bounds__(kSuperBlock, 4) k_part_bin2(KeySpan ks, ModParams mp,
                                                               uint64_t *__restrict__ pos_out,
                                                               uint32_t *__restrict__ runs, SegMap sm,
-                                                              size_t ntiles) {
+                                                              size_t ntiles, uint16_t *__restrict__ slots) {
     constexpr int TB = kSuperBlock;
     constexpr int kHalfKeys = TB * kPartKPT;          // 8192
     constexpr int kTileKeys = 2 * kHalfKeys;          // 16384
@@ -649,6 +652,36 @@ __global__ void __launch_bounds__(kSuperBlock, 4) k_part_bin2(KeySpan ks, ModPar
             // (two registers per entry instead of one)
             asm volatile("" : "+v"(brA[q]), "+v"(brB[q]));
             if (q % 6 == 5) __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (SLOTS) {
+            // key 8 tid + j of half A and 8192 + 8 tid + j of half B: their
+            // sorted index per hash, one non-temporal 16-B store per half and
+            // hash (read once, by the combine, after pass 2)
+            uint16_t *sl = slots + tile * 3 * (size_t)kTileKeys + kPartKPT * tid;
+            if constexpr (FULL) {
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+                for (int h = 0; h < 3; h++) {
+                    // byte slots: 4 | slot, so (odd << 14) | (even >> 2)
+                    const v4u wa = {lshl_or(brA[3 + h], 14, brA[h] >> 2), lshl_or(brA[9 + h], 14, brA[6 + h] >> 2),
+                                    lshl_or(brA[15 + h], 14, brA[12 + h] >> 2),
+                                    lshl_or(brA[21 + h], 14, brA[18 + h] >> 2)};
+                    const v4u wb = {lshl_or(brB[3 + h], 14, brB[h] >> 2), lshl_or(brB[9 + h], 14, brB[6 + h] >> 2),
+                                    lshl_or(brB[15 + h], 14, brB[12 + h] >> 2),
+                                    lshl_or(brB[21 + h], 14, brB[18 + h] >> 2)};
+                    __builtin_nontemporal_store(wa, reinterpret_cast<v4u *>(sl + h * kTileKeys));
+                    __builtin_nontemporal_store(wb, reinterpret_cast<v4u *>(sl + h * kTileKeys + kHalfKeys));
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < kPartKPT; j++) {
+#pragma unroll
+                    for (int h = 0; h < 3; h++) {
+                        if (live(0, j)) sl[h * kTileKeys + j] = (uint16_t)(brA[3 * j + h] >> 2);
+                        if (live(1, j)) sl[h * kTileKeys + kHalfKeys + j] = (uint16_t)(brB[3 * j + h] >> 2);
+                    }
+                }
+            }
         }
         lds_barrier();  // the histogram is read: the image is free
 
@@ -1347,51 +1380,63 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
 // multiplies: with bytes b0..b3 (0/1 at bits 0, 8, 16, 24),
 // (b * 0x01020408) >> 24 puts b_i at bit i and every other partial product
 // below bit 24 or above bit 31 (no carries: those bits are distinct).
-constexpr int kCombineKeys = 8;  // keys per thread
+constexpr int kCombineKeys = 8;  // keys per thread (and pass: super-tiles take two)
 template <int TILE_KEYS, int kCombineBlock>
 __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
     const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, size_t n,
     uint64_t *__restrict__ out, size_t nw, StackTable rows) {
     constexpr int kTilePos = 3 * TILE_KEYS;
-    static_assert(kCombineBlock * kCombineKeys == TILE_KEYS, "8 keys per thread");
+    constexpr int kPasses = TILE_KEYS / (kCombineBlock * kCombineKeys);
+    static_assert(kPasses * kCombineBlock * kCombineKeys == TILE_KEYS, "8 keys per thread and pass");
     __shared__ __attribute__((aligned(16))) uint8_t s_r[kTilePos];
     const size_t tile = blockIdx.x;
     const size_t tile0 = tile * TILE_KEYS;
     const int tile_keys = (int)min((size_t)TILE_KEYS, n - tile0);
-    const int k0 = kCombineKeys * (int)threadIdx.x;  // this thread's first key in the tile
-    const uint4 *sl = reinterpret_cast<const uint4 *>(slots + tile * 3 * TILE_KEYS + k0);
-    const uint4 va = sl[0], vb = sl[TILE_KEYS / 8], vc = sl[2 * (TILE_KEYS / 8)];
+    uint4 va[kPasses], vb[kPasses], vc[kPasses];
+#pragma unroll
+    for (int ps = 0; ps < kPasses; ps++) {
+        const int k0 = kCombineKeys * ((int)threadIdx.x + ps * kCombineBlock);
+        const uint4 *sl = reinterpret_cast<const uint4 *>(slots + tile * 3 * TILE_KEYS + k0);
+        va[ps] = sl[0];
+        vb[ps] = sl[TILE_KEYS / 8];
+        vc[ps] = sl[2 * (TILE_KEYS / 8)];
+    }
     const uint4 *src = reinterpret_cast<const uint4 *>(res + tile * (size_t)kTilePos);
     for (int q = threadIdx.x; q < kTilePos / 16; q += kCombineBlock)
         reinterpret_cast<uint4 *>(s_r)[q] = src[q];
     __syncthreads();
-    // live keys of a short last tile; past them the slots are stale
-    const uint32_t a[4] = {va.x, va.y, va.z, va.w}, b[4] = {vb.x, vb.y, vb.z, vb.w},
-                   c[4] = {vc.x, vc.y, vc.z, vc.w};
-    uint32_t hit[kCombineKeys];
 #pragma unroll
-    for (int i = 0; i < kCombineKeys; i++) {
-        const int sh = 16 * (i & 1);
-        const uint32_t sa = (a[i / 2] >> sh) & 0xFFFFu, sb = (b[i / 2] >> sh) & 0xFFFFu,
-                       sc = (c[i / 2] >> sh) & 0xFFFFu;
-        hit[i] = k0 + i < tile_keys ? (uint32_t)(s_r[min(sa, (uint32_t)kTilePos - 1)] &
-                                                 s_r[min(sb, (uint32_t)kTilePos - 1)] &
-                                                 s_r[min(sc, (uint32_t)kTilePos - 1)])
-                                    : 0u;
-    }
-    // bytes of the tile's rows that hold keys: whole 64-key words, so the last
-    // word of a short tile gets its zero bits too
-    if (k0 >= ((tile_keys + 63) & ~63)) return;
-    const uint32_t lo = hit[0] | (hit[1] << 8) | (hit[2] << 16) | (hit[3] << 24);
-    const uint32_t hi = hit[4] | (hit[5] << 8) | (hit[6] << 16) | (hit[7] << 24);
-    const size_t byte0 = tile0 / 8 + threadIdx.x;
+    for (int ps = 0; ps < kPasses; ps++) {
+        const int k0 = kCombineKeys * ((int)threadIdx.x + ps * kCombineBlock);  // this pass's first key
+        // live keys of a short last tile; past them the slots are stale
+        const uint32_t a[4] = {va[ps].x, va[ps].y, va[ps].z, va[ps].w},
+                       b[4] = {vb[ps].x, vb[ps].y, vb[ps].z, vb[ps].w},
+                       c[4] = {vc[ps].x, vc[ps].y, vc[ps].z, vc[ps].w};
+        uint32_t hit[kCombineKeys];
 #pragma unroll
-    for (int j = 0; j < kMaxStack; j++) {
-        if (j < rows.nf) {
-            const uint32_t bl = ((lo >> j) & 0x01010101u) * 0x01020408u;
-            const uint32_t bh = ((hi >> j) & 0x01010101u) * 0x01020408u;
-            const uint32_t byte = (bl >> 24) | ((bh >> 20) & 0xF0u);
-            reinterpret_cast<uint8_t *>(out + (size_t)rows.row[j] * nw)[byte0] = (uint8_t)byte;
+        for (int i = 0; i < kCombineKeys; i++) {
+            const int sh = 16 * (i & 1);
+            const uint32_t sa = (a[i / 2] >> sh) & 0xFFFFu, sb = (b[i / 2] >> sh) & 0xFFFFu,
+                           sc = (c[i / 2] >> sh) & 0xFFFFu;
+            hit[i] = k0 + i < tile_keys ? (uint32_t)(s_r[min(sa, (uint32_t)kTilePos - 1)] &
+                                                     s_r[min(sb, (uint32_t)kTilePos - 1)] &
+                                                     s_r[min(sc, (uint32_t)kTilePos - 1)])
+                                        : 0u;
+        }
+        // bytes of the tile's rows that hold keys: whole 64-key words, so the
+        // last word of a short tile gets its zero bits too
+        if (k0 >= ((tile_keys + 63) & ~63)) continue;
+        const uint32_t lo = hit[0] | (hit[1] << 8) | (hit[2] << 16) | (hit[3] << 24);
+        const uint32_t hi = hit[4] | (hit[5] << 8) | (hit[6] << 16) | (hit[7] << 24);
+        const size_t byte0 = tile0 / 8 + threadIdx.x + ps * kCombineBlock;
+#pragma unroll
+        for (int j = 0; j < kMaxStack; j++) {
+            if (j < rows.nf) {
+                const uint32_t bl = ((lo >> j) & 0x01010101u) * 0x01020408u;
+                const uint32_t bh = ((hi >> j) & 0x01010101u) * 0x01020408u;
+                const uint32_t byte = (bl >> 24) | ((bh >> 20) & 0xF0u);
+                reinterpret_cast<uint8_t *>(out + (size_t)rows.row[j] * nw)[byte0] = (uint8_t)byte;
+            }
         }
     }
 }
@@ -1461,7 +1506,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
     uint64_t *__restrict__ out, size_t nw, StackTable rows, RouteTable rt,
     int32_t *__restrict__ first, int32_t *__restrict__ page, size_t ntiles) {
     constexpr int kTilePos = 3 * TILE_KEYS;
-    static_assert(BLOCK * kCombineKeys == TILE_KEYS, "8 keys per thread");
+    constexpr int kPasses = TILE_KEYS / (BLOCK * kCombineKeys);  // super-tiles: two
+    static_assert(kPasses * BLOCK * kCombineKeys == TILE_KEYS, "8 keys per thread and pass");
     extern __shared__ int32_t s_fences[];
     __shared__ __attribute__((aligned(16))) uint8_t s_r[kTilePos];
     __shared__ int32_t s_lo[kMaxStack], s_hi[kMaxStack];
@@ -1511,24 +1557,29 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
             }
         }
     }
-    const int k0 = kCombineKeys * (int)threadIdx.x;  // this thread's first key in a tile
+    const int kt = kCombineKeys * (int)threadIdx.x;  // this thread's first key in a tile's pass
     const bool vec_out = ((reinterpret_cast<uintptr_t>(first) | reinterpret_cast<uintptr_t>(page)) & 15) == 0;
     for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t tile0 = tile * TILE_KEYS;
         const int tile_keys = (int)min((size_t)TILE_KEYS, ks.n - tile0);
-        const uint4 *sl = reinterpret_cast<const uint4 *>(slots + tile * 3 * TILE_KEYS + k0);
-        const uint4 va = sl[0], vb = sl[TILE_KEYS / 8], vc = sl[2 * (TILE_KEYS / 8)];
+        // pass ps's keys: 8 tid + 8 BLOCK ps .. + 7; their slots and the keys
+        // (pass 0's loads in flight across the staging below)
+        const uint4 *sl = reinterpret_cast<const uint4 *>(slots + tile * 3 * TILE_KEYS + kt);
+        uint4 va = sl[0], vb = sl[TILE_KEYS / 8], vc = sl[2 * (TILE_KEYS / 8)];
         int32_t key[kCombineKeys];
-        if (LAYOUT == KEYS_PACKED && tile_keys == TILE_KEYS) {
-            const int4 *kv = reinterpret_cast<const int4 *>(ks.base) + (tile0 + k0) / 4;
-            const int4 x = kv[0], y = kv[1];
-            key[0] = x.x; key[1] = x.y; key[2] = x.z; key[3] = x.w;
-            key[4] = y.x; key[5] = y.y; key[6] = y.z; key[7] = y.w;
-        } else {
+        auto load_keys = [&](int k0) {
+            if (LAYOUT == KEYS_PACKED && tile_keys == TILE_KEYS) {
+                const int4 *kv = reinterpret_cast<const int4 *>(ks.base) + (tile0 + k0) / 4;
+                const int4 x = kv[0], y = kv[1];
+                key[0] = x.x; key[1] = x.y; key[2] = x.z; key[3] = x.w;
+                key[4] = y.x; key[5] = y.y; key[6] = y.z; key[7] = y.w;
+            } else {
 #pragma unroll
-            for (int i = 0; i < kCombineKeys; i++)
-                key[i] = k0 + i < tile_keys ? load_key<LAYOUT>(ks, tile0 + k0 + i) : 0;
-        }
+                for (int i = 0; i < kCombineKeys; i++)
+                    key[i] = k0 + i < tile_keys ? load_key<LAYOUT>(ks, tile0 + k0 + i) : 0;
+            }
+        };
+        load_keys(kt);
         __syncthreads();  // the previous tile's result bytes are no longer read
         // the tile's result bytes: every load issued before any LDS store (a
         // load-store loop waited for each; loaded before the barrier, they
@@ -1542,6 +1593,16 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
         for (int j = 0; j < kResPer; j++)
             if ((int)threadIdx.x + j * BLOCK < kResVec) reinterpret_cast<uint4 *>(s_r)[threadIdx.x + j * BLOCK] = rv[j];
         __syncthreads();
+#pragma unroll
+        for (int ps = 0; ps < kPasses; ps++) {
+        const int k0 = kt + ps * kCombineKeys * BLOCK;  // this pass's first key
+        if (ps > 0) {
+            const uint4 *sp = sl + ps * BLOCK;  // 8 u16 per thread: BLOCK vectors per pass
+            va = sp[0];
+            vb = sp[TILE_KEYS / 8];
+            vc = sp[2 * (TILE_KEYS / 8)];
+            load_keys(k0);
+        }
         const uint32_t a[4] = {va.x, va.y, va.z, va.w}, b[4] = {vb.x, vb.y, vb.z, vb.w},
                        c[4] = {vc.x, vc.y, vc.z, vc.w};
         uint32_t cand_lo = 0, cand_hi = 0;  // byte i: key i's candidate runs (bit r: filter and range)
@@ -1645,7 +1706,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
         // 64-key words), run r's byte = bit r of the 8 keys' masks
         if (k0 < ((tile_keys + 63) & ~63)) {
             const uint32_t lo = cand_lo, hi = cand_hi;
-            const size_t byte0 = tile0 / 8 + threadIdx.x;
+            const size_t byte0 = tile0 / 8 + threadIdx.x + ps * BLOCK;
 #pragma unroll
             for (int r = 0; r < kMaxStack; r++) {
                 if (r < nf) {
@@ -1656,6 +1717,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
                 }
             }
         }
+        }  // passes
     }
 }
 
@@ -1674,6 +1736,8 @@ hipError_t launch_bin_probe512(const KeySpan &ks, const ModParams &mp, const Par
 // pass 1 of a build on super-tiles (bloom_pass1_super.hip)
 hipError_t launch_bin_super(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                             hipStream_t stream);
+hipError_t launch_bin_super_probe(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                                  uint16_t *slots, hipStream_t stream);  // bloom_pass1_super_probe.hip
 hipError_t launch_bin_probe1024(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                                 uint16_t *slots, hipStream_t stream);
 // pass 2 of the probes (bloom_probe.hip, bloom_probe_ladder.hip) and the combine
@@ -1826,16 +1890,17 @@ hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const Partition
 
 // Pass 1 on super-tiles (k_part_bin2): builds whose geometry plan_build gave
 // kSuperTileKeys (segments of m < 2^32, more than kSuperMinBins of them).
-template <int MK>
+template <int MK, bool SLOTS>
 hipError_t launch_bin_super_mk(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
-                               const SegMap &sm, hipStream_t stream) {
+                               const SegMap &sm, uint16_t *slots, hipStream_t stream) {
     const bool cols = runs_as_columns(ws);
     uint32_t *runs = cols ? ws.run_starts : ws.run_rows;
     const size_t g = (size_t)device_cu_count();
     const unsigned grid = (unsigned)(ws.ntiles < g ? ws.ntiles : g);
     const bool entry16 = ks.layout == KEYS_ENTRY && (reinterpret_cast<uintptr_t>(ks.base) & 15) == 0;
 #define SUPER_L(L, C) \
-    k_part_bin2<L, C, MK, (int)kSuperMaxBins><<<grid, kSuperBlock, 0, stream>>>(ks, mp, ws.pos, runs, sm, ws.ntiles)
+    k_part_bin2<L, C, MK, (int)kSuperMaxBins, SLOTS><<<grid, kSuperBlock, 0, stream>>>(ks, mp, ws.pos, runs, sm, \
+                                                                                     ws.ntiles, slots)
     if (ks.layout == KEYS_PACKED) {
         if (cols) SUPER_L(KEYS_PACKED, true); else SUPER_L(KEYS_PACKED, false);
     } else if (entry16) {
@@ -1849,13 +1914,14 @@ hipError_t launch_bin_super_mk(const KeySpan &ks, const ModParams &mp, const Par
     return launch_runs_transpose(ws, stream);
 }
 
-inline hipError_t launch_bin_super_impl(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
-                                        hipStream_t stream) {
-    if (ws.nbins > 4095) return hipErrorInvalidValue;
+template <bool SLOTS>
+hipError_t launch_bin_super_impl(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
+                                 uint16_t *slots, hipStream_t stream) {
+    if (ws.nbins > kSuperMaxBins || (SLOTS && !slots)) return hipErrorInvalidValue;
     SegMap sm{};
-    switch (pass1_plan(mp, ws, false, &sm)) {
-        case kModP2: return launch_bin_super_mk<kModP2>(ks, mp, ws, sm, stream);
-        case kModFast: return launch_bin_super_mk<kModFast>(ks, mp, ws, sm, stream);
+    switch (pass1_plan(mp, ws, SLOTS, &sm)) {
+        case kModP2: return launch_bin_super_mk<kModP2, SLOTS>(ks, mp, ws, sm, slots, stream);
+        case kModFast: return launch_bin_super_mk<kModFast, SLOTS>(ks, mp, ws, sm, slots, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1868,6 +1934,7 @@ hipError_t launch_bin(const KeySpan &ks, const ModParams &mp, const PartitionWor
                       uint16_t *slots, hipStream_t stream) {
     const bool big = tile_keys_of(ws) == 2 * kPartTileKeys;
     if constexpr (SLOTS) {
+        if (tile_keys_of(ws) == kSuperTileKeys) return launch_bin_super_probe(ks, mp, ws, slots, stream);
         return big ? launch_bin_probe1024(ks, mp, ws, slots, stream)
                    : launch_bin_probe512(ks, mp, ws, slots, stream);
     } else {
@@ -2045,6 +2112,10 @@ hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *word
                 return launch_apply_g<MODE, 4, TK, 1, 3>(ws, m, words, nw32, merge, res, st, stream);
             return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
         }
+    } else if constexpr (MODE == kApplyStack) {
+        // a segment stack on super-tiles (plan_stack: 1,024-4,095 segments,
+        // runs of 12-48 entries): four lanes per tile, two vectors per lane
+        if (tile_keys_of(ws) == kSuperTileKeys) return launch_stack_nf<4, (int)kSuperTileKeys, 3>(ws, m, res, st, stream);
     }
     return tile_keys_of(ws) == 2 * kPartTileKeys
                ? launch_apply_tk<MODE, 2 * (int)kPartTileKeys>(ws, m, words, nw32, merge, res, st,

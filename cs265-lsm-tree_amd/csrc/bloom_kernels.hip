@@ -659,6 +659,9 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
     ws->seg_bits = (uint32_t)best_w;
     ws->nbins = (size_t)(m_max / best_w);
     ws->magic = best_magic;
+    // many short runs (the f = 10 tree: 1,250 segments, ~20 entries per
+    // 8192-key tile): pass 1 on super-tiles (k_part_bin2 with the slot plane)
+    ws->tile_keys = ws->nbins >= kSuperMinBins && ws->nbins <= kSuperMaxBins ? (uint32_t)kSuperTileKeys : 0u;
     return true;
 }
 

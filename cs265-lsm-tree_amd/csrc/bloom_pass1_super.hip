@@ -6,7 +6,7 @@ namespace bloomhip {
 
 hipError_t launch_bin_super(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace &ws,
                             hipStream_t stream) {
-    return launch_bin_super_impl(ks, mp, ws, stream);
+    return launch_bin_super_impl<false>(ks, mp, ws, nullptr, stream);
 }
 
 }  // namespace bloomhip

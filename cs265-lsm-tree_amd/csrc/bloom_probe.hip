@@ -9,8 +9,10 @@ namespace bloomhip {
 hipError_t launch_combine(const PartitionWorkspace &ws, const uint8_t *res, const uint16_t *slots,
                           size_t n, uint64_t *out, size_t nw, const StackTable &rows,
                           hipStream_t stream) {
-    constexpr int kBig = 2 * (int)kPartTileKeys, kSmall = (int)kPartTileKeys;
-    if (tile_keys_of(ws) == 2 * kPartTileKeys)
+    constexpr int kBig = 2 * (int)kPartTileKeys, kSmall = (int)kPartTileKeys, kSuper = (int)kSuperTileKeys;
+    if (tile_keys_of(ws) == kSuperTileKeys)  // super-tiles: two passes of 8 keys per thread
+        k_probe_combine<kSuper, 1024><<<(unsigned)ws.ntiles, 1024, 0, stream>>>(res, slots, n, out, nw, rows);
+    else if (tile_keys_of(ws) == 2 * kPartTileKeys)
         k_probe_combine<kBig, kBig / kCombineKeys>
             <<<(unsigned)ws.ntiles, kBig / kCombineKeys, 0, stream>>>(res, slots, n, out, nw, rows);
     else
@@ -59,18 +61,25 @@ hipError_t launch_combine_route(const PartitionWorkspace &ws, const uint8_t *res
     // while two copies of the fences and the tile's result bytes fit the
     // LDS, else one (a second round of workgroups would start only when the
     // first has walked all of its tiles)
-    const size_t per_wg = lds + 3 * (size_t)kBig + 1024;
+    const size_t per_wg = lds + 3 * (size_t)tile_keys_of(ws) + 1024;
     const size_t cap = (size_t)device_cu_count() * (2 * per_wg <= kLdsBitmapBytes ? 2 : 1);
     const unsigned grid = (unsigned)(ws.ntiles < cap ? ws.ntiles : cap);
 #define COMBINE_ROUTE(TK, L)                                                                      \
     k_probe_combine_route<TK, TK / kCombineKeys, L><<<grid, TK / kCombineKeys, lds, stream>>>(    \
         res, slots, ks, out, nw, rows, rt, first, page, ws.ntiles)
-    const bool big = tile_keys_of(ws) == 2 * kPartTileKeys;
+    const bool big = tile_keys_of(ws) == 2 * kPartTileKeys, super = tile_keys_of(ws) == kSuperTileKeys;
+    constexpr int kSuper = (int)kSuperTileKeys;
+#define COMBINE_ROUTE_SUPER(L)                                                                    \
+    k_probe_combine_route<kSuper, 1024, L><<<grid, 1024, lds, stream>>>(                          \
+        res, slots, ks, out, nw, rows, rt, first, page, ws.ntiles)
     if (ks.layout == KEYS_PACKED) {
-        if (big) COMBINE_ROUTE(kBig, KEYS_PACKED); else COMBINE_ROUTE(kSmall, KEYS_PACKED);
+        if (super) COMBINE_ROUTE_SUPER(KEYS_PACKED);
+        else if (big) COMBINE_ROUTE(kBig, KEYS_PACKED); else COMBINE_ROUTE(kSmall, KEYS_PACKED);
     } else {
-        if (big) COMBINE_ROUTE(kBig, KEYS_STRIDED); else COMBINE_ROUTE(kSmall, KEYS_STRIDED);
+        if (super) COMBINE_ROUTE_SUPER(KEYS_STRIDED);
+        else if (big) COMBINE_ROUTE(kBig, KEYS_STRIDED); else COMBINE_ROUTE(kSmall, KEYS_STRIDED);
     }
+#undef COMBINE_ROUTE_SUPER
 #undef COMBINE_ROUTE
     return hipGetLastError();
 }

@@ -373,6 +373,17 @@ def test_ladder_stack_tiny_ragged_and_strided(coracle, n):
     _stack_case(coracle, ms, rand_keys(n, 91 + n), stride=8, seed=4)
 
 
+@pytest.mark.parametrize("n", [1, 63, 16_383, 16_385, 40_001])
+def test_stacked_probe_super_tiles_ragged_and_strided(coracle, n):
+    """The f = 10 tree's stack (1,250 segments: pass 1 on 16,384-key
+    super-tiles with the slot plane, pass 2 at 16,384 keys per tile, the
+    two-pass combine) on batches below one super-tile and one key past it,
+    packed and entry_t keys."""
+    ms = [5_120_000 * 10**i for i in range(3)]
+    _stack_case(coracle, ms, rand_keys(n, 95 + n), seed=5)
+    _stack_case(coracle, ms, rand_keys(n, 96 + n), stride=8, seed=6)
+
+
 def test_stacked_probe_auto_and_strided(coracle):
     """AUTO stacks a divisible group at >= 2^18 keys; AoS entry_t keys."""
     ms = [655_360 * 4**i for i in range(5)]

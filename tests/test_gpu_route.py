@@ -327,3 +327,20 @@ def test_route_fused_duplicate_fences_and_edges(coracle):
     wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     assert (first == 1).any() and (page[first == 2] > 0).any()
+
+
+@pytest.mark.parametrize("n", [100_001, 16_385])
+def test_route_fused_on_super_tiles(coracle, n):
+    """The f = 10 tree's filter sizes (m = 5.12M * 10^i) over runs of 5,120 *
+    10^i keys (1,000 bits per key): one segment stack of 1,250 segments, so
+    the probe sorts 16,384-key super-tiles and the combine with routing fused
+    in takes each super-tile in two passes; a ragged batch and one key past a
+    super-tile, against the oracle, the path asserted."""
+    runs, refs = build_runs([5_120, 51_200, 512_000], bpe=1000.0, seed=6, probe=bh.PROBE_STACKED)
+    assert [m for _, m in refs] == [5_120_000 * 10**i for i in range(3)]
+    gets = get_keys(refs, n, 17)
+    path, (cand, first, page) = routed_by(runs, lambda: bh.route_gets(runs, gets))
+    assert path == "fused"
+    wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
+    assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
+    assert (first >= 0).sum() > n // 4
