@@ -1593,6 +1593,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
         for (int j = 0; j < kResPer; j++)
             if ((int)threadIdx.x + j * BLOCK < kResVec) reinterpret_cast<uint4 *>(s_r)[threadIdx.x + j * BLOCK] = rv[j];
         __syncthreads();
+        // (unrolled: a loop over the two passes of a super-tile spilled 44
+        // VGPRs; the 512-lane strided-key variant spills 2 either way)
 #pragma unroll
         for (int ps = 0; ps < kPasses; ps++) {
         const int k0 = kt + ps * kCombineKeys * BLOCK;  // this pass's first key
@@ -1943,8 +1945,6 @@ hipError_t launch_bin(const KeySpan &ks, const ModParams &mp, const PartitionWor
     }
 }
 
-// Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
-// must be opted into per kernel).
 // The segment stack's pass 2 on persistent workgroups (round 5): member j's
 // window of segment b starts at word (b * sw) mod mw_j, periodic in b with
 // period P_j = mw_j / gcd(sw, mw_j) (the f = 10 tree at w = 409,600 bits:
@@ -1984,6 +1984,8 @@ inline void stack_stride(size_t nbins, uint32_t seg_words, size_t lds, StackTabl
     st.keep_mask = mask;
 }
 
+// Launches pass 2 (build or probe) with S/8 bytes of dynamic LDS (> 64 KiB
+// must be opted into per kernel).
 template <int MODE, int G, int TK, int DEPTH = kApplyDepth, int WALK = 0, int NF = 0, int LK = 0>
 hipError_t launch_apply_g(const PartitionWorkspace &ws, uint64_t m, uint32_t *words,
                           uint64_t nw32, int merge, uint8_t *res, const StackTable &st,
