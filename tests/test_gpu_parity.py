@@ -319,10 +319,10 @@ def _stack_case(coracle, ms, probe_keys, strategies=None, stride=4, seed=0):
         lo, hi = j * 1000, min((j + 1) * 1000, probe_keys.size)
         if lo < hi:
             probe_keys[lo:hi] = keys[:hi - lo]   # some hits per filter
-    if stride == 8:
-        aos = np.zeros((probe_keys.size, 2), dtype=np.int32)
+    if stride in (8, 12):
+        aos = np.zeros((probe_keys.size, stride // 4), dtype=np.int32)
         aos[:, 0] = probe_keys
-        got = bh.test_batch(filters, aos.reshape(-1), n=probe_keys.size, stride=8)
+        got = bh.test_batch(filters, aos.reshape(-1), n=probe_keys.size, stride=stride)
     else:
         got = bh.test_batch(filters, probe_keys)
     for j, (m, w) in enumerate(refs):
@@ -378,10 +378,11 @@ def test_stacked_probe_super_tiles_ragged_and_strided(coracle, n):
     """The f = 10 tree's stack (1,250 segments: pass 1 on 16,384-key
     super-tiles with the slot plane, pass 2 at 16,384 keys per tile, the
     two-pass combine) on batches below one super-tile and one key past it,
-    packed and entry_t keys."""
+    packed keys, entry_t keys and 12-byte records (the strided loads)."""
     ms = [5_120_000 * 10**i for i in range(3)]
     _stack_case(coracle, ms, rand_keys(n, 95 + n), seed=5)
     _stack_case(coracle, ms, rand_keys(n, 96 + n), stride=8, seed=6)
+    _stack_case(coracle, ms, rand_keys(n, 97 + n), stride=12, seed=7)
 
 
 def test_stacked_probe_auto_and_strided(coracle):
