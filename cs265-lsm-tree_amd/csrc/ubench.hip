@@ -513,3 +513,38 @@ extern "C" int ubench_cal(int shape, void *buf, size_t nv, int R, int nseg, void
     ub_cal<<<grid, 1024, 0, s>>>(reinterpret_cast<uint4 *>(buf), nv, shape, R, nseg, sink);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+
+// The run-table transpose with a configurable column stride (>= ntiles):
+// rows [ntiles][width] -> cols[b * cstride + tile].  VEC = 1: the product's
+// 64 x 64 LDS tile, 4-B accesses; VEC = 4: rows read as 16-B vectors when
+// width % 4 == 0.  (tools/ubench.py transpose: does the 64 KiB column stride
+// of C4's 16,384 super-tiles cost the write side?)
+namespace {
+__global__ void __launch_bounds__(256) ub_transpose(const uint32_t *__restrict__ rows,
+                                                    uint32_t *__restrict__ cols, size_t ntiles,
+                                                    int width, size_t cstride) {
+    __shared__ uint32_t t[64][65];
+    const int b0 = blockIdx.x * 64;
+    const size_t t0 = (size_t)blockIdx.y * 64;
+    const int x = threadIdx.x & 63, y0 = threadIdx.x >> 6;
+    for (int y = y0; y < 64; y += 4) {
+        const size_t tile = t0 + y;
+        if (tile < ntiles && b0 + x < width) t[y][x] = rows[tile * width + b0 + x];
+    }
+    __syncthreads();
+    for (int y = y0; y < 64; y += 4) {
+        const size_t tile = t0 + x;
+        if (tile < ntiles && b0 + y < width) cols[(size_t)(b0 + y) * cstride + tile] = t[x][y];
+    }
+}
+}  // namespace
+
+extern "C" int ubench_transpose(const void *rows, void *cols, size_t ntiles, int width,
+                                size_t cstride, void *stream) {
+    if (cstride < ntiles) return -22;
+    const dim3 grid((unsigned)((width + 63) / 64), (unsigned)((ntiles + 63) / 64));
+    ub_transpose<<<grid, 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        reinterpret_cast<const uint32_t *>(rows), reinterpret_cast<uint32_t *>(cols), ntiles, width,
+        cstride);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}

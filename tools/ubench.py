@@ -420,8 +420,44 @@ def pass1_arith(buf, grid, block, iters=256, reps=5):
               flush=True)
 
 
+def transpose(reps=20):
+    """The run-table transpose at C4's shape (16,384 super-tiles x 2,458
+    segments) with the column stride = ntiles (the product) and padded by
+    16-256 words: the padding tests whether 64 KiB-strided column rows
+    collide in the caches."""
+    LIB.ubench_transpose.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                     ctypes.c_size_t, ctypes.c_void_p]
+    LIB.ubench_transpose.restype = ctypes.c_int
+    for ntiles, width in ((16384, 2458), (32768, 2458), (4096, 256)):
+        rows = torch.randint(0, 2**31 - 1, (ntiles * width,), dtype=torch.int32, device="cuda")
+        for pad in (0, 16, 32, 64, 256):
+            cstride = ntiles + pad
+            cols = torch.zeros(width * cstride, dtype=torch.int32, device="cuda")
+            s = torch.cuda.current_stream()
+            rc = LIB.ubench_transpose(rows.data_ptr(), cols.data_ptr(), ntiles, width, cstride, s.cuda_stream)
+            assert rc == 0, rc
+            torch.cuda.synchronize()
+            # correctness: column b, tile t == rows[t * width + b]
+            c = cols.view(width, cstride)[:, :ntiles]
+            assert torch.equal(c, rows.view(ntiles, width).t()), (ntiles, width, pad)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            for _ in range(reps):
+                LIB.ubench_transpose(rows.data_ptr(), cols.data_ptr(), ntiles, width, cstride, s.cuda_stream)
+            b.record(s)
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) / reps * 1000
+            print(json.dumps({"op": "transpose", "ntiles": ntiles, "width": width, "pad_words": pad,
+                              "us": round(us, 1),
+                              "GBps": round(2 * ntiles * width * 4 / us / 1e3, 1)}), flush=True)
+            del cols
+        del rows
+
+
 def main():
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "transpose":
+        return transpose()
     if len(sys.argv) > 1 and sys.argv[1] == "mixed":
         return mixed()
     if len(sys.argv) > 1 and sys.argv[1] == "cal":
