@@ -539,6 +539,39 @@ __global__ void __launch_bounds__(256) ub_transpose(const uint32_t *__restrict__
 }
 }  // namespace
 
+// variant 2: every load of the tile issued before any LDS store (clamped
+// addresses, no load under a branch), the stores likewise; TR tile rows.
+template <int TR>
+__global__ void __launch_bounds__(256) ub_transpose2(const uint32_t *__restrict__ rows,
+                                                     uint32_t *__restrict__ cols, size_t ntiles,
+                                                     int width, size_t cstride) {
+    __shared__ uint32_t t[TR][65];
+    constexpr int kPer = TR / 4;
+    const int b0 = blockIdx.x * 64;
+    const size_t t0 = (size_t)blockIdx.y * TR;
+    const int x = threadIdx.x & 63, y0 = threadIdx.x >> 6;
+    uint32_t v[kPer];
+    const int bx = min(b0 + x, width - 1);
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+        const size_t tile = min(t0 + y0 + 4 * i, ntiles - 1);
+        v[i] = rows[tile * width + bx];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; i++) t[y0 + 4 * i][x] = v[i];
+    __syncthreads();
+    // writes: lane x takes tile t0 + x (+ 64 per half for TR = 128), row b0 + y
+#pragma unroll
+    for (int h = 0; h < TR / 64; h++) {
+        const size_t tile = t0 + h * 64 + x;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int y = y0 + 4 * i;
+            if (tile < ntiles && b0 + y < width) cols[(size_t)(b0 + y) * cstride + tile] = t[h * 64 + x][y];
+        }
+    }
+}
+
 extern "C" int ubench_transpose(const void *rows, void *cols, size_t ntiles, int width,
                                 size_t cstride, void *stream) {
     if (cstride < ntiles) return -22;
@@ -546,5 +579,17 @@ extern "C" int ubench_transpose(const void *rows, void *cols, size_t ntiles, int
     ub_transpose<<<grid, 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
         reinterpret_cast<const uint32_t *>(rows), reinterpret_cast<uint32_t *>(cols), ntiles, width,
         cstride);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int ubench_transpose2(int tr, const void *rows, void *cols, size_t ntiles, int width,
+                                 size_t cstride, void *stream) {
+    if (cstride < ntiles || (tr != 64 && tr != 128)) return -22;
+    const dim3 grid((unsigned)((width + 63) / 64), (unsigned)((ntiles + tr - 1) / tr));
+    auto r = reinterpret_cast<const uint32_t *>(rows);
+    auto c = reinterpret_cast<uint32_t *>(cols);
+    auto s = reinterpret_cast<hipStream_t>(stream);
+    if (tr == 64) ub_transpose2<64><<<grid, 256, 0, s>>>(r, c, ntiles, width, cstride);
+    else ub_transpose2<128><<<grid, 256, 0, s>>>(r, c, ntiles, width, cstride);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

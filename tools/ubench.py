@@ -428,9 +428,33 @@ def transpose(reps=20):
     LIB.ubench_transpose.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                      ctypes.c_size_t, ctypes.c_void_p]
     LIB.ubench_transpose.restype = ctypes.c_int
+    LIB.ubench_transpose2.argtypes = [ctypes.c_int] + LIB.ubench_transpose.argtypes
+    LIB.ubench_transpose2.restype = ctypes.c_int
+    variants = [("product", 0), ("loads first, 64 rows", 64), ("loads first, 128 rows", 128)]
     for ntiles, width in ((16384, 2458), (32768, 2458), (4096, 256)):
         rows = torch.randint(0, 2**31 - 1, (ntiles * width,), dtype=torch.int32, device="cuda")
-        for pad in (0, 16, 32, 64, 256):
+        for name, tr in variants:
+            cols = torch.zeros(width * ntiles, dtype=torch.int32, device="cuda")
+            s = torch.cuda.current_stream()
+            call = (lambda: LIB.ubench_transpose(rows.data_ptr(), cols.data_ptr(), ntiles, width, ntiles,
+                                                 s.cuda_stream)) if tr == 0 else \
+                (lambda: LIB.ubench_transpose2(tr, rows.data_ptr(), cols.data_ptr(), ntiles, width, ntiles,
+                                               s.cuda_stream))
+            assert call() == 0
+            torch.cuda.synchronize()
+            assert torch.equal(cols.view(width, ntiles), rows.view(ntiles, width).t()), (name, ntiles)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            for _ in range(reps):
+                call()
+            b.record(s)
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) / reps * 1000
+            print(json.dumps({"op": "transpose", "variant": name, "ntiles": ntiles, "width": width,
+                              "us": round(us, 1), "GBps": round(2 * ntiles * width * 4 / us / 1e3, 1)}),
+                  flush=True)
+            del cols
+        for pad in (0, 32):
             cstride = ntiles + pad
             cols = torch.zeros(width * cstride, dtype=torch.int32, device="cuda")
             s = torch.cuda.current_stream()
