@@ -778,6 +778,8 @@ constexpr int kTransposeBlock = 256;
 // ---------------------------------------------------------------------------
 
 constexpr int kApplyBlock = 1024;
+// pass 2's prologue: loads per thread in flight while an LDS image is staged
+constexpr int kStageBatch = 4;
 constexpr int kApplyDepth = 2;  // lane-group loads per wave per batch
 
 // Lanes per tile for pass 2, from the average run length L = tile entries /
@@ -869,15 +871,31 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             const uint32_t mw = st.mwords[j];
             const uint32_t start = (uint32_t)(((uint64_t)b * seg_words) % mw);
             const uint4 *src = reinterpret_cast<const uint4 *>(st.words[j]);
-            for (int i = tix; i < (int)seg_words / 4; i += BLOCK) {
-                uint32_t wi = start + 4u * (uint32_t)i;
-                if (wi >= mw) wi -= mw;
-                const uint4 v = src[wi / 4];
-                uint32_t *dst = seg + (size_t)(4 * i) * nf + j;
-                dst[0] = v.x;
-                dst[nf] = v.y;
-                dst[2 * nf] = v.z;
-                dst[3 * nf] = v.w;
+            const int nvec = (int)seg_words / 4;
+            // kStageBatch vectors per thread in flight before their LDS
+            // stores; past the end a lane reloads its own first vector (no
+            // load under a branch, and no one address every lane hits); a
+            // load-store loop waited for each load in turn
+            for (int i0 = tix; i0 < nvec; i0 += kStageBatch * BLOCK) {
+                uint4 v[kStageBatch];
+#pragma unroll
+                for (int k = 0; k < kStageBatch; k++) {
+                    const int ik = i0 + k * BLOCK;
+                    uint32_t wi = start + 4u * (uint32_t)(ik < nvec ? ik : i0);
+                    if (wi >= mw) wi -= mw;
+                    v[k] = src[wi / 4];
+                }
+#pragma unroll
+                for (int k = 0; k < kStageBatch; k++) {
+                    const int i = i0 + k * BLOCK;
+                    if (i < nvec) {
+                        uint32_t *dst = seg + (size_t)(4 * i) * nf + j;
+                        dst[0] = v[k].x;
+                        dst[nf] = v[k].y;
+                        dst[2 * nf] = v[k].z;
+                        dst[3 * nf] = v[k].w;
+                    }
+                }
             }
         }
     } else if constexpr (MODE == kApplyLadder) {
@@ -914,6 +932,8 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             const uint32_t hj = tj - L.s - L.u;
             return (aj << hj) | ((xs >> L.u) & ((1u << hj) - 1u));
         };
+        // (one load per iteration: batching these loads, as the segment
+        // stack's staging does, made C3's probe 0.170 -> 0.180 ms)
         auto stage_direct = [&]() {
             for (uint32_t j = 0; j < K; j++) {
                 const uint4 *src = reinterpret_cast<const uint4 *>(st.words[j]);
