@@ -1421,9 +1421,18 @@ __global__ void __launch_bounds__(kCombineBlock) k_probe_combine(
         vb[ps] = sl[TILE_KEYS / 8];
         vc[ps] = sl[2 * (TILE_KEYS / 8)];
     }
+    // the tile's result bytes: every load issued before any LDS store, at
+    // clamped indices (no load under a branch; a load-store loop waited for
+    // each load in turn)
     const uint4 *src = reinterpret_cast<const uint4 *>(res + tile * (size_t)kTilePos);
-    for (int q = threadIdx.x; q < kTilePos / 16; q += kCombineBlock)
-        reinterpret_cast<uint4 *>(s_r)[q] = src[q];
+    constexpr int kResVec = kTilePos / 16, kResPer = (kResVec + kCombineBlock - 1) / kCombineBlock;
+    uint4 rv[kResPer];
+#pragma unroll
+    for (int j = 0; j < kResPer; j++) rv[j] = src[min((int)threadIdx.x + j * kCombineBlock, kResVec - 1)];
+#pragma unroll
+    for (int j = 0; j < kResPer; j++)
+        if ((int)threadIdx.x + j * kCombineBlock < kResVec)
+            reinterpret_cast<uint4 *>(s_r)[threadIdx.x + j * kCombineBlock] = rv[j];
     __syncthreads();
 #pragma unroll
     for (int ps = 0; ps < kPasses; ps++) {
