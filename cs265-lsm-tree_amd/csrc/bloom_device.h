@@ -192,6 +192,9 @@ constexpr uint32_t kBinShift = 19;  // 8192 segments << 19 < 2^32
 // runs[b * ntiles + tile]; COLS = false: into the tile-major
 // runs[tile * nbins + b], for k_runs_transpose (large tables).
 constexpr int kModFast = 0, kModWide = 1, kModP2 = 2, kModLadder = 3, kModLadder0 = 4;
+// plan_build's one-member ladder with the block relabelled to (x >> 24) % d
+// (bloom_math.h mod_p2_hi24; ladder0_relabel): C2 and C5
+constexpr int kModLadder0R = 5;
 
 // The bin (segment) of one raw hash and its pass-1 entry (the position's low
 // kEntryBits bits, or the ladder's packed form), by reduction MK: pass 1's
@@ -231,6 +234,20 @@ __device__ __forceinline__ void bin_entry(uint64_t raw, const ModParams &mp, con
             b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
             ent = (a << sm.shift) | __builtin_amdgcn_ubfe(xl, 0, sm.shift);
         }
+    } else if constexpr (MK == kModLadder0R) {
+        // as kModLadder0 with a' = (x >> 24) % d for a = (x >> t) % d: one
+        // shift and one v_sad_u8 instead of an alignbit, a shift and the sad
+        // (pass 2 maps image block a' back to a, ladder0_block)
+        const uint32_t xl = (uint32_t)raw;
+        if constexpr (MINW >= 6) {
+            const uint32_t lo = __builtin_amdgcn_ubfe(xl, 0, sm.shift);
+            b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
+            ent = lshl_or_s(mod_p2_hi24(raw, mp), sm.shift, lo);
+        } else {
+            const uint32_t a = mod_p2_hi24(raw, mp);
+            b = __builtin_amdgcn_ubfe(xl, sm.shift, sm.lad_u);
+            ent = (a << sm.shift) | __builtin_amdgcn_ubfe(xl, 0, sm.shift);
+        }
     } else if constexpr (MK == kModP2) {
         const uint32_t xl = (uint32_t)raw;
         const uint32_t r = mod_p2_hi(raw, mp);
@@ -247,9 +264,22 @@ __device__ __forceinline__ void bin_entry(uint64_t raw, const ModParams &mp, con
     }
 }
 
-// NO_TILE_STORE (micro-benchmarks only): skip the sorted tile's stores.
+// ABL (micro-benchmarks only, tools/ubench.py p1abl: the pass's cost by
+// stage): 0 the whole tile; 1 hash + bin and entry only; 2 + the rank
+// atomics; 3 + the scan and the run table; 4 + the scatter; 5 + the packing,
+// without the sorted tile's stores.  A stage's unconsumed results go to one
+// store that only an impossible value takes.
+//
+// HC > 1: HC copies of the histogram, counter (bin b, copy c) at word
+// b * HC + c, lane l counting in copy c = l % HC.  A wave's 32-lane half
+// then spreads its rank atomics and offset reads over the banks by copy
+// class (bank 4 (b mod 8) + c at HC = 4: 8 lanes over 8 banks instead of
+// 32 over 32, a smaller expected worst bank); the scan runs over the
+// copies bin-major, so bin b's run of the tile is still one contiguous
+// range (the concatenation of its copies' ranks).  One bin per scanning
+// thread (nbins < TB).
 template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4,
-          bool NO_TILE_STORE = false>
+          int ABL = 0, int HC = 1>
 __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                                                        uint64_t *__restrict__ pos_out,
                                                        uint32_t *__restrict__ runs, SegMap sm,
@@ -257,20 +287,22 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
     constexpr int kTileKeys = TB * kPartKPT;
     constexpr int kTilePos = 3 * kTileKeys;
     constexpr int kMaxB = MAXB ? MAXB : TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
-    constexpr int kScanPer = (kMaxB + 1 + TB - 1) / TB;  // scan entries per thread, at most
+    constexpr int kScanPer = HC > 1 ? HC : (kMaxB + 1 + TB - 1) / TB;  // scan entries per thread, at most
     static_assert(4 * kTilePos <= (1 << 17) && kTilePos < (1 << 16) &&
-                      ((uint64_t)(kMaxB - 1) << kBinShift) < (1ull << 32),
+                      ((uint64_t)((kMaxB + 1) * HC - 2) << kBinShift) < (1ull << 32),
                   "packed rank fields (bin nbins, never incremented, may wrap to 0)");
+    static_assert(HC == 1 || (HC == 4 && kMaxB < TB), "copies: one bin per scanning thread");
     // static LDS even for the 96 KiB of an 8192-key tile (gfx950 takes it);
     // dynamic LDS or a pointer to it made the compiler spill registers here
     __shared__ __attribute__((aligned(16))) uint32_t s_sorted[kTilePos];
-    __shared__ uint32_t s_hist[kMaxB + 1];
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[(kMaxB + 1) * HC];
     __shared__ uint32_t s_wsum[TB / 64];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int nb = (int)sm.nbins;
-    const int per = (nb + 1 + TB - 1) / TB;  // this launch's scan entries per thread
+    const int per = HC > 1 ? HC : (nb + 1 + TB - 1) / TB;  // this launch's scan entries per thread
+    const uint32_t hc = (uint32_t)lane & (HC - 1);          // this lane's histogram copy
     int32_t kcur[kPartKPT], knext[kPartKPT];
 
     // One tile.  FULL (every tile but a short last one) makes the key count a
@@ -284,7 +316,7 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
         const int tile_keys = FULL ? (int)kTileKeys : (int)min((size_t)kTileKeys, ks.n - tile0);
         auto live = [&](int j) { return FULL || kPartKPT * tid + j < tile_keys; };
 #pragma clang loop unroll(disable) vectorize(disable)
-        for (int b = tid; b <= nb; b += TB) s_hist[b] = (uint32_t)b << kBinShift;
+        for (int b = tid; b < (nb + 1) * HC; b += TB) s_hist[b] = (uint32_t)b << kBinShift;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
 
         // 1. positions -> (segment, rank in segment) and the entry; the ranks
@@ -302,7 +334,8 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                     uint32_t b, e;
                     bin_entry<MK, MINW>(raw, mp, sm, b, e);
                     ent[3 * j + h] = e;
-                    br[3 * j + h] = atomicAdd(&s_hist[b], 4u);
+                    if constexpr (ABL == 1) br[3 * j + h] = b;
+                    else br[3 * j + h] = atomicAdd(&s_hist[HC > 1 ? b * HC + hc : b], 4u);
                 }
             } else {
 #pragma unroll
@@ -310,14 +343,70 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
             }
         }
         lds_barrier();
+        // (ablation: the stage's results consumed by one impossible store)
+        auto consume = [&]() {
+            uint32_t x = 0;
+#pragma unroll
+            for (int q = 0; q < 3 * kPartKPT; q++) x ^= br[q] + ent[q];
+            if (x == 0x9E3779B9u) reinterpret_cast<uint32_t *>(pos_out)[tile * kTileKeys + tid] = x;
+        };
+        if constexpr (ABL == 1 || ABL == 2) {
+            if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
+            consume();
+            return;
+        }
 
         // 2. exclusive scan of the nbins+1 counts (the extra slot is 0 and
         //    receives the tile total); thread t owns [t*per, t*per + per).
         //    Waves that own no bin (C2: waves 5-7 of 8) skip it: nobody
         //    reads their wave sums, which come after every live bin.
-        const bool scan_wave = wave * 64 * per <= nb;  // uniform per wave
+        const bool scan_wave = wave * 64 * (HC > 1 ? 1 : per) <= nb;  // uniform per wave
         uint32_t local[kScanPer];  // 4 * count of bin b
         uint32_t tsum = 0, incl = 0;
+        if constexpr (HC > 1) {
+            // thread t owns bin t's HC counters (one 16-B read; read again
+            // after the barrier rather than kept in registers)
+            (void)local;
+            // counter b * HC + c holds its (b * HC + c) << kBinShift bias
+            // plus 4 * count: the four biases differ by 1 << kBinShift
+            auto counts = [&](const uint4 &c4, uint32_t &x, uint32_t &y, uint32_t &z) {
+                const uint32_t q0 = (uint32_t)(tid * HC) << kBinShift;
+                x = c4.x - q0;
+                y = c4.y - q0 - (1u << kBinShift);
+                z = c4.z - q0 - (2u << kBinShift);
+                return c4.w - q0 - (3u << kBinShift);
+            };
+            if (scan_wave) {
+                if (tid <= nb) {
+                    uint32_t x, y, z;
+                    const uint32_t w = counts(*reinterpret_cast<const uint4 *>(s_hist + tid * HC), x, y, z);
+                    tsum = x + y + z + w;
+                }
+                incl = wave_incl_scan(tsum);
+                if (lane == 63) s_wsum[wave] = incl;
+            }
+            lds_barrier();
+            if (scan_wave) {
+                uint32_t run = incl - tsum;
+                for (int w = 0; w < wave; w++) run += s_wsum[w];
+                if (tid <= nb) {
+                    const uint32_t q0 = (uint32_t)(tid * HC) << kBinShift;
+                    uint32_t x, y, z;
+                    (void)counts(*reinterpret_cast<const uint4 *>(s_hist + tid * HC), x, y, z);
+                    uint4 o;
+                    o.x = run - q0;
+                    o.y = run + x - q0 - (1u << kBinShift);
+                    o.z = run + x + y - q0 - (2u << kBinShift);
+                    o.w = run + x + y + z - q0 - (3u << kBinShift);
+                    *reinterpret_cast<uint4 *>(s_hist + tid * HC) = o;
+                    const uint32_t pk = (run >> 2) | (((run + tsum) >> 2) << 16);
+                    if (tid < nb) {
+                        if constexpr (COLS) runs[(size_t)tid * ntiles + tile] = pk;
+                        else runs[tile * (size_t)nb + tid] = pk;
+                    }
+                }
+            }
+        } else {
         if (scan_wave) {
 #pragma unroll
             for (int q = 0; q < kScanPer; q++) {
@@ -351,8 +440,13 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                 }
             }
         }
+        }
         lds_barrier();
         if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
+        if constexpr (ABL == 3) {
+            consume();
+            return;
+        }
 
         // 3. scatter into the LDS image sorted by segment, one hash at a time:
         //    its kPartKPT offset reads first (one wait), then the writes.
@@ -392,6 +486,7 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
             }
         }
         lds_barrier();
+        if constexpr (ABL == 4) return;
         // 4. the sorted tile goes out packed, three entries per u64, as 16-B
         //    stores: thread t packs entries 6v .. 6v+5 for its vectors v.  In
         //    a short tile the entries past its end are stale, masked so they
@@ -415,7 +510,7 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
             v[r] = make_uint4(lshl_or(e[1], 21, e[0]), lshl_or(e[2], 10, e[1] >> 11),
                               lshl_or(e[4], 21, e[3]), lshl_or(e[5], 10, e[4] >> 11));
         }
-        if constexpr (!NO_TILE_STORE) {
+        if constexpr (ABL == 0) {
 #pragma unroll
             for (int r = 0; r < kStores; r++) dst[r * TB + tid] = v[r];
         } else {
@@ -1341,13 +1436,17 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     __syncthreads();
 
     if constexpr (MODE == kApplyBuildL) {
-        // block a of the image (2^s bits) is the bitmap's bits a << t | b << s
+        // block a of the image (2^s bits) is the bitmap's bits a << t | b << s;
+        // with the relabelled pass 1 (LadderTable::rinv != 0) image block a'
+        // is the bitmap's block ladder0_block(a', b)
         const uint32_t ls = st.lad.s, lt = st.lad.t[0];
         const uint32_t vpb = 1u << (ls - 7);  // 16-B vectors per block
         const uint4 *seg4 = reinterpret_cast<const uint4 *>(seg);
         uint4 *w4 = reinterpret_cast<uint4 *>(words);
         for (uint32_t q = tix; q < st.lad.d * vpb; q += BLOCK) {
-            const uint32_t a = q >> (ls - 7), i = q & (vpb - 1u);
+            uint32_t a = q >> (ls - 7);
+            const uint32_t i = q & (vpb - 1u);
+            if (st.lad.rinv) a = ladder0_block(a, (uint32_t)b, ls, st.lad.d, st.lad.rinv);
             uint4 *dq = w4 + (((size_t)a << (lt - 7)) + ((size_t)b << (ls - 7)) + i);
             uint4 v = seg4[q];
             if (merge_existing) {
@@ -1852,7 +1951,8 @@ inline int pass1_plan(const ModParams &mp, const PartitionWorkspace &ws, bool sl
     if (ws.lad_u) {  // ladder stack: bins are hash bits [s, s + u) (plan_ladder)
         if (!mp.fast || !mp.p2 || sm.shift + sm.lad_u + sm.lad_hb != mp.p2t) return -1;
         sm.scaled_shift = sm.shift + sm.lad_u;
-        mk = sm.lad_hb == 0 && !slots ? kModLadder0 : kModLadder;  // plan_build's one-member ladder
+        // plan_build's one-member ladder, relabelled where 24 lies in [s, t]
+        mk = sm.lad_hb == 0 && !slots ? (ladder0_relabel(mp, ws) ? kModLadder0R : kModLadder0) : kModLadder;
     } else if (wide) {
         mk = kModWide;
     } else if (p2_pass1(mp, sm)) {
@@ -1903,6 +2003,13 @@ hipError_t launch_bin_tb(const KeySpan &ks, const ModParams &mp, const Partition
         case kModLadder0:
             if constexpr (!SLOTS) {
                 bin_launch_layout<SLOTS, TB, kModLadder0>(ks, mp, ws, runs, sm, cols, slots, stream);
+                break;
+            } else {
+                return hipErrorInvalidValue;
+            }
+        case kModLadder0R:
+            if constexpr (!SLOTS) {
+                bin_launch_layout<SLOTS, TB, kModLadder0R>(ks, mp, ws, runs, sm, cols, slots, stream);
                 break;
             } else {
                 return hipErrorInvalidValue;

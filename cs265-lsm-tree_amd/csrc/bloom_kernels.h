@@ -114,6 +114,23 @@ struct PartitionWorkspace {
 };
 
 
+// Whether a build on plan_build's one-member ladder (bins = hash bits
+// [s, t), m = d << t) takes the relabelled block a' = (x >> 24) % d in pass 1
+// (bloom_math.h mod_p2_hi24: one instruction less per position) and pass 2
+// maps it back (ladder0_block): when s <= 24 <= t, so the hash bits [24, t)
+// are bin bits (C2: s = 17, t = 25; C5: s = 18, t = 27).
+inline bool ladder0_relabel(const ModParams &mp, const PartitionWorkspace &ws) {
+    return ws.lad_u && ws.lad_hb == 0 && mp.p2 && ws.lad_s <= 24 && mp.p2t >= 24;
+}
+// 2^-(t-24) mod d (d odd) for ladder0_block.
+inline uint32_t ladder0_inv(const ModParams &mp) {
+    uint32_t p = 1;
+    for (uint32_t i = 24; i < mp.p2t; i++) p = p * 2 % mp.p2d;
+    for (uint32_t v = 1; v < mp.p2d; v++)
+        if (p * v % mp.p2d == 1) return v;
+    return 1;  // d = 1 (not a p2 form)
+}
+
 inline SegMap seg_map_of(const PartitionWorkspace &ws) {
     if (ws.lad_u) return SegMap{ws.lad_s, 0, (uint32_t)ws.nbins, 0, 0, ws.lad_u, ws.lad_hb};
     return SegMap{ws.sub_shift - 1, ws.magic, (uint32_t)ws.nbins, 0, 0, 0, 0};
@@ -229,6 +246,9 @@ struct LadderTable {
     // images may fill all of the LDS.
     uint32_t ctup;
     uint32_t tmagic;
+    // plan_build's one-member ladder (a build's pass 2, kApplyBuildL) after
+    // the relabelled pass 1 (ladder0_relabel): 2^-(t-24) mod d, else 0
+    uint32_t rinv;
 };
 
 struct StackTable {

@@ -195,6 +195,37 @@ BH_HD uint32_t mod_p2_hi(uint64_t x, const ModParams &p) {
 #endif
 }
 
+// (x >> 24) % d for the p2 form (d | 255): x >> 24 = xh * 2^8 + (xl >> 24)
+// and 2^8 = 1 (mod d), so it is congruent to the sum of xh's four bytes plus
+// xl's top byte: one shift and ONE v_sad_u8 (s <= 5 * 255), then the same
+// mulhi / mad as mod_p2_hi -- 4 instructions against 5, the alignbit gone.
+// plan_build's one-member ladder takes it when 24 lies in [s, t] (the hash
+// bits [24, t) are then bin bits): a' = (x >> 24) % d = (2^(t-24) a + c) % d
+// with a = (x >> t) % d and c = bits [24, t) of x, so a' is a relabelling of
+// a for every bin, which pass 2 undoes block by block (ladder0_block).
+BH_HD uint32_t mod_p2_hi24(uint64_t x, const ModParams &p) {
+    const uint32_t xh = (uint32_t)(x >> 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t s = __builtin_amdgcn_sad_u8(xh, 0u, (uint32_t)x >> 24);
+    const uint32_t q = __umulhi(s, p.p2M);
+    return (uint32_t)((int)s + __mul24((int)q, -(int)p.p2d));
+#else
+    const uint32_t s = (xh & 0xFFu) + ((xh >> 8) & 0xFFu) + ((xh >> 16) & 0xFFu) + (xh >> 24) +
+                       ((uint32_t)x >> 24);
+    const uint32_t q = (uint32_t)(((uint64_t)s * p.p2M) >> 32);
+    return s - q * p.p2d;
+#endif
+}
+
+// The bitmap block a = (x >> t) % d of image block a' = (x >> 24) % d in bin
+// b of plan_build's one-member ladder with the relabelled pass 1 (s <= 24 <=
+// t): c = bits [24, t) of x = b >> (24 - s), and a' = (2^(t-24) a + c) % d,
+// so a = (a' - c) * 2^-(t-24) mod d (d odd).  inv = 2^-(t-24) mod d.
+BH_HD uint32_t ladder0_block(uint32_t ap, uint32_t b, uint32_t s, uint32_t d, uint32_t inv) {
+    const uint32_t c = (b >> (24 - s)) % d;
+    return ((ap + d - c) * inv) % d;
+}
+
 // x % m for m = d << t (p.p2): ((x >> t) % d) << t | (x mod 2^t).
 BH_HD uint32_t mod_p2(uint64_t x, const ModParams &p) {
     const uint32_t r = mod_p2_hi(x, p);

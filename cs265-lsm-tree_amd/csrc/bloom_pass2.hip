@@ -17,6 +17,7 @@ hipError_t launch_part_apply(const ModParams &mp, uint32_t *words, const Partiti
         st.lad.u = ws.lad_u;
         st.lad.d = mp.p2d;
         st.lad.t[0] = mp.p2t;
+        st.lad.rinv = ladder0_relabel(mp, ws) ? ladder0_inv(mp) : 0u;
         return launch_apply<kApplyBuildL>(ws, mp.m, words, nw32, merge_existing, nullptr, st,
                                           stream);
     }

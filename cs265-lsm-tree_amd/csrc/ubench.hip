@@ -222,6 +222,7 @@ extern "C" int ubench_pass1_arith(int nf, const uint64_t *ms, int grid, int bloc
         case kModP2: ub_pass1_arith<kModP2><<<grid, block, 0, s>>>(mp, sm, iters, sink); break;
         case kModLadder: ub_pass1_arith<kModLadder><<<grid, block, 0, s>>>(mp, sm, iters, sink); break;
         case kModLadder0: ub_pass1_arith<kModLadder0><<<grid, block, 0, s>>>(mp, sm, iters, sink); break;
+        case kModLadder0R: ub_pass1_arith<kModLadder0R><<<grid, block, 0, s>>>(mp, sm, iters, sink); break;
         default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -288,6 +289,39 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     }
         UB_P2(5001, 512, 511, 4, 2) UB_P2(5003, 512, 511, 6, 3)
 #undef UB_P2
+        // 5100 + ABL: the product's C2 pass 1 (plan_build's one-member
+        // ladder, 4096-key tiles, three workgroups per CU) cut after a
+        // stage (k_part_bin's ABL): the ablation ladder of tools/ubench.py p1abl
+#define UB_ABL(A)                                                                                 \
+    case 5100 + A: {                                                                             \
+        SegMap sm{};                                                                             \
+        if (pass1_plan(mp, ws, false, &sm) != kModLadder0R || ws.tile_keys != 4096 ||           \
+            ws.nbins > 511 || !runs_as_columns(ws))                                              \
+            return -22;                                                                          \
+        const unsigned g = (unsigned)std::min<size_t>(ws.ntiles, (size_t)device_cu_count() * 3); \
+        k_part_bin<KEYS_PACKED, false, true, 512, kModLadder0R, 511, 6, A>                       \
+            <<<g, 512, 0, s>>>(ks, mp, ws.pos, ws.run_starts, sm, ws.ntiles, nullptr);           \
+        e = hipGetLastError();                                                                   \
+        break;                                                                                   \
+    }
+        UB_ABL(0) UB_ABL(1) UB_ABL(2) UB_ABL(3) UB_ABL(4) UB_ABL(5)
+#undef UB_ABL
+        // 5110 + ABL: the same with four histogram copies (k_part_bin's HC = 4,
+        // capacity 256 bins so three workgroups still fit a CU)
+#define UB_HC(A)                                                                                  \
+    case 5110 + A: {                                                                             \
+        SegMap sm{};                                                                             \
+        if (pass1_plan(mp, ws, false, &sm) != kModLadder0R || ws.tile_keys != 4096 ||           \
+            ws.nbins > 256 || !runs_as_columns(ws))                                              \
+            return -22;                                                                          \
+        const unsigned g = (unsigned)std::min<size_t>(ws.ntiles, (size_t)device_cu_count() * 3); \
+        k_part_bin<KEYS_PACKED, false, true, 512, kModLadder0R, 256, 6, A, 4>                    \
+            <<<g, 512, 0, s>>>(ks, mp, ws.pos, ws.run_starts, sm, ws.ntiles, nullptr);           \
+        e = hipGetLastError();                                                                   \
+        break;                                                                                   \
+    }
+        UB_HC(0) UB_HC(2) UB_HC(3) UB_HC(5)
+#undef UB_HC
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;
@@ -403,8 +437,8 @@ extern "C" int ubench_ladder(int variant, int tile_keys, const void *keys, size_
                 if (cols) k_part_bin<KEYS_PACKED, false, true, 1024, kModLadder, 1023, 4><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
                 else k_part_bin<KEYS_PACKED, false, false, 1024, kModLadder, 1023, 4><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
             } else {
-                if (cols) k_part_bin<KEYS_PACKED, false, true, 1024, kModLadder, 1023, 4, true><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
-                else k_part_bin<KEYS_PACKED, false, false, 1024, kModLadder, 1023, 4, true><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
+                if (cols) k_part_bin<KEYS_PACKED, false, true, 1024, kModLadder, 1023, 4, 5><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
+                else k_part_bin<KEYS_PACKED, false, false, 1024, kModLadder, 1023, 4, 5><<<g, 1024, 0, s>>>(ks, mp, ws.pos, rt, sm, ws.ntiles, nullptr);
             }
             e = hipGetLastError();
             if (e == hipSuccess && !cols) e = launch_runs_transpose(ws, s);

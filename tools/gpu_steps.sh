@@ -41,6 +41,13 @@ for s in ${STEPS//,/ }; do
     sq_part_c4) run sq_part_c4_a 200 timeout -s KILL 190 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d "$OUT/sq_part_c4_a" -o pmc --output-format csv -- python tools/ubench.py part_c4 || exit 1
              run sq_part_c4_b 200 timeout -s KILL 190 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace -d "$OUT/sq_part_c4_b" -o pmc --output-format csv -- python tools/ubench.py part_c4 || exit 1 ;;
     ub_stack) run ub_stack 300 python tools/ubench.py stack || exit 1 ;;
+    build_ab_c2) run build_ab_c2 400 python tools/build_ab.py 5 c2 || exit 1 ;;
+    build_ab_c5) run build_ab_c5 400 python tools/build_ab.py 3 c5 || exit 1 ;;
+    build_ab_f10) run build_ab_f10 400 python tools/build_ab.py 3 f10 || exit 1 ;;
+    ub_p1abl) run ub_p1abl 300 python tools/ubench.py p1abl || exit 1 ;;
+    ub_p1tail) run ub_p1tail 300 python tools/ubench.py p1tail || exit 1 ;;
+    sq_p1abl) run sq_p1abl_a 200 timeout -s KILL 190 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d "$OUT/sq_p1abl_a" -o pmc --output-format csv -- python tools/ubench.py p1abl || exit 1
+              run sq_p1abl_b 200 timeout -s KILL 190 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace -d "$OUT/sq_p1abl_b" -o pmc --output-format csv -- python tools/ubench.py p1abl || exit 1 ;;
     pcie) run pcie 120 python tools/pcie_probe.py || exit 1 ;;
     ub_ladder) run ub_ladder 300 python tools/ubench.py ladder || exit 1 ;;
     ub_chunks) run ub_chunks 300 env UB_LADDER=2,201,202,203,204,206,208 python tools/ubench.py ladder || exit 1 ;;

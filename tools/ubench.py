@@ -57,13 +57,14 @@ def _events(fn, reps):
     return a.elapsed_time(b) / reps
 
 
-def _part_setup(n, bpe):
-    """Keys, geometry and buffers of the product's partition build of n keys."""
+def _part_setup(n, bpe, m=None):
+    """Keys, geometry and buffers of the product's partition build of n keys
+    (into m bits, else n * bpe as Run::Run sizes it)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "cs265-lsm-tree_amd"))
     import bloomhip as bh
     keys = torch.from_numpy(bh.gen_puts(13141, n)).cuda()
-    m = bh.m_bits(n, bpe)
+    m = m or bh.m_bits(n, bpe)
     geo = np.zeros(4, dtype=np.uint64)
     assert LIB.ubench_part_geometry(n, m, geo.ctypes.data) == 0
     nbins, seg_bits, tk, ntiles = (int(x) for x in geo)
@@ -172,6 +173,60 @@ def p2_ab(variants, n=16_777_216, bpe=10.0, rounds=3, reps=50):
     for v, ts in res.items():
         print(json.dumps({"op": "pass 2 A/B", **geo, "variant": v, "us": ts, "min_us": min(ts)}),
               flush=True)
+
+
+def p1_ablation(n=16_777_216, bpe=10.0, rounds=3, reps=50):
+    """C2's pass 1 cut after each stage (ubench_part 5100 + ABL, k_part_bin's
+    ABL): 1 hash + bin/entry, 2 + rank atomics, 3 + scan and run table,
+    4 + scatter, 5 + packing (no tile stores), 0 = the whole pass.  Variant
+    5100 must give the product's bitmap through the product's pass 2;
+    interleaved rounds."""
+    run, words, geo = _part_setup(n, bpe)
+    assert run(0) == 0 and run(1) == 0
+    torch.cuda.synchronize()
+    ref = words.clone()
+    words.zero_()
+    assert run(5100) == 0 and run(1) == 0
+    torch.cuda.synchronize()
+    print(json.dumps({"check": "ablation variant 5100 bitmap == product", "ok": bool(torch.equal(ref, words))}),
+          flush=True)
+    names = {5101: "hash + bin/entry", 5102: "+ rank atomics", 5103: "+ scan, run table",
+             5105: "+ scatter + packing (no stores)", 5100: "whole pass 1", 0: "product pass 1",
+             5112: "HC=4: + rank atomics", 5113: "HC=4: + scan", 5115: "HC=4: + scatter + packing",
+             5110: "HC=4: whole pass 1"}
+    # (ABL 4, the scatter without the packing, is left out: nothing reads the
+    # scattered image, so the compiler drops the scatter and the entries)
+    words.zero_()
+    if run(5110) == 0:
+        run(1)
+        torch.cuda.synchronize()
+        print(json.dumps({"check": "HC=4 variant 5110 bitmap == product", "ok": bool(torch.equal(ref, words))}),
+              flush=True)
+    _prewarm(run, 0)
+    res = {v: [] for v in names}
+    for _ in range(rounds):
+        for v in names:
+            assert run(v) == 0
+            res[v].append(round(_events(lambda: run(v), reps) * 1e3, 2))
+    for v, ts in res.items():
+        print(json.dumps({"op": "pass 1 ablation", **geo, "variant": v, "stage": names[v], "us": ts,
+                          "min_us": min(ts)}), flush=True)
+
+
+def p1_tail(m=167_772_160, reps=50):
+    """The product's pass 1 at whole and partial last rounds: C2's 4096
+    tiles are 5 1/3 rounds of the 768 resident workgroups (3 per CU); the
+    filter stays C2's (m = 5 << 25), only the key count changes."""
+    for ntiles in (3840, 4096, 4352, 4608, 3840, 4096):
+        n = ntiles * 4096
+        run, words, geo = _part_setup(n, 0.0, m)
+        _prewarm(run, 0, 0.3)
+        ts = [round(_events(lambda: run(0), reps) * 1e3, 2) for _ in range(3)]
+        print(json.dumps({"op": "pass 1 tail", "tiles": ntiles, "rounds": round(ntiles / 768, 3),
+                          "us": ts, "min_us": min(ts), "us_per_round": round(min(ts) / (ntiles / 768), 2)}),
+              flush=True)
+        del run, words
+        torch.cuda.empty_cache()
 
 
 def stack_ablation(levels_sel=(0, 1, 2, 3, 4)):
@@ -500,6 +555,10 @@ def main():
         size = {"p2ab": (16_777_216, 10.0, 50), "p2ab_c5": (67_108_864, 10.0, 20),
                 "p2ab_c4": (268_435_456, 12.0, 5)}[sys.argv[1]]
         return p2_ab(vs, *size)
+    if len(sys.argv) > 1 and sys.argv[1] == "p1abl":
+        return p1_ablation()
+    if len(sys.argv) > 1 and sys.argv[1] == "p1tail":
+        return p1_tail()
     if len(sys.argv) > 1 and sys.argv[1] == "part":
         return part_phases()
     if len(sys.argv) > 1 and sys.argv[1] == "part_c5":
