@@ -353,8 +353,12 @@ def probe_c3(torch, bh):
 def route_c3(torch, bh, workload="c3"):
     """§8f row 1: batched GET routing of C3's 16.8M GETs over the five level
     runs (range check + filter probe + newest candidate + page index), all
-    outputs device-resident; workload "f10": the same GETs over the f = 10
-    tree's three level runs (13,875 fences)."""
+    outputs device-resident, the answer packed one u32 per GET
+    (bloomhip_route_gets_packed: run << 28 | page); workload "f10": the same
+    GETs over the f = 10 tree's three level runs (13,875 fences).  The
+    candidate rows and the packed answers of the last timed call are checked
+    against the oracle's pins (bo_route, tests/golden/pins.json)."""
+    import numpy as np
     from bloomhip import workloads as W
     gets, levels = W.c3_runs() if workload == "c3" else W.f10_runs()
     runs = []
@@ -365,20 +369,33 @@ def route_c3(torch, bh, workload="c3"):
     n = gets.size
     dgets = torch.from_numpy(gets).cuda()
     dc = torch.empty((len(runs), (n + 63) // 64), dtype=torch.int64, device="cuda")
-    df = torch.empty(n, dtype=torch.int32, device="cuda")
-    dp = torch.empty(n, dtype=torch.int32, device="cuda")
+    dr = torch.empty(n, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
     wall, n_pre = time_leg(
-        lambda: bh.route_gets(runs, dgets, cand=dc, first=df, page=dp, stream=s), torch)
-    routed = int((df >= 0).sum().item())
+        lambda: bh.route_gets_packed(runs, dgets, cand=dc, route=dr, stream=s), torch)
+    route = dr.cpu().numpy().view(np.uint32)
+    routed = int((route != bh.ROUTE_NONE).sum())
+    pins = load_pins()
+    pin = None
+    if pins:
+        pin = pins["oracle"].get("route_c3") if workload == "c3" else \
+            (pins["oracle"].get("f10") or {}).get("route")
+    sha_ok = None
+    if pin:
+        sha_ok = (hashlib.sha256(dc.cpu().numpy().view(np.uint64).tobytes()).hexdigest() == pin["cand_sha256"]
+                  and hashlib.sha256(route.tobytes()).hexdigest() == pin["route_sha256"])
+        if not sha_ok:
+            log(f"route {workload}: OUTPUTS DIFFER from the oracle pins")
     # SURVEY §8(d)'s probe bytes (keys, every filter, a bit per key and run)
-    # plus the routing outputs (first and page: 8 B per key)
-    algo = 4 * n + sum((m + 7) // 8 for _, _, m in levels) + len(runs) * n // 8 + 8 * n
+    # plus the routing output (the packed answer: 4 B per key)
+    algo = 4 * n + sum((m + 7) // 8 for _, _, m in levels) + len(runs) * n // 8 + 4 * n
     return {"gkeys_s": round(n / (wall * 1e9), 3), "wall_ms": round(wall * 1e3, 4),
             "timed_calls": LEG_MIN_CALLS, "prewarm_calls": n_pre,
+            "output": "packed u32 per GET (bloomhip_route_gets_packed)",
             "keys_with_candidate": routed, "algorithmic_bytes": algo,
             "achieved_GBps": round(algo / wall / 1e9, 1),
-            "frac": round(algo / wall / 1e9 / HBM_PEAK_GBPS, 4)}
+            "frac": round(algo / wall / 1e9 / HBM_PEAK_GBPS, 4),
+            "route_sha_match": sha_ok}
 
 
 def probe_c3_sharded(torch, bh, dist, rank, world, coll_dev):
@@ -496,8 +513,20 @@ def compact_fanin(torch, bh):
         got[0] = bh.compact(druns, drop_tombstones=True, filter=f, out=dout)
     t, n_pre = time_leg(call, torch)
     n_out = int(got[0].shape[0])
+    # the last timed call's merged run and filter against the oracle's pins
+    # (bo_compact, src/merge.cpp:17-35, and the filter over its keys)
+    pins = load_pins()
+    pin = pins["oracle"].get("compact_fanin4") if pins else None
+    sha_ok = None
+    if pin:
+        merged = got[0].cpu().numpy() if hasattr(got[0], "cpu") else got[0]
+        sha_ok = (hashlib.sha256(merged.tobytes()).hexdigest() == pin["merged_sha256"]
+                  and hashlib.sha256(f.words().tobytes()).hexdigest() == pin["filter_sha256"])
+        if not sha_ok:
+            log("compaction fan-in 4: OUTPUTS DIFFER from the oracle pins")
     algo = 8 * total + 8 * n_out + (m + 7) // 8  # runs in, merged run out, the new filter
     return {"gentries_s": round(total / t / 1e9, 3), "ms": round(t * 1e3, 3),
+            "merged_and_filter_sha_match": sha_ok,
             "timed_calls": LEG_MIN_CALLS, "prewarm_calls": n_pre,
             "entries_in": total, "entries_out": n_out, "algorithmic_bytes": algo,
             "achieved_GBps": round(algo / t / 1e9, 1), "frac": round(algo / t / 1e9 / HBM_PEAK_GBPS, 4),
@@ -993,6 +1022,9 @@ def main():
         "c5_eight_bitmaps_sha": (extras.get("c5_eight_runs") or {}).get("verified_vs_oracle"),
         "f10_build_bitmap_sha": ((extras.get("f10") or {}).get("build") or {}).get("verified_vs_oracle"),
         "f10_hits_sha": ((extras.get("f10") or {}).get("probe") or {}).get("hits_sha_match"),
+        "route_c3_sha": (extras.get("route_c3") or {}).get("route_sha_match"),
+        "f10_route_sha": ((extras.get("f10") or {}).get("route") or {}).get("route_sha_match"),
+        "compact_fanin4_sha": (extras.get("compact_fanin4") or {}).get("merged_and_filter_sha_match"),
     }
     print(json.dumps(line), flush=True)
     if dist:

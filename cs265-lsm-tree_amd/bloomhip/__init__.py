@@ -60,7 +60,7 @@ EXPORTED_SYMBOLS = (
     "bloomhip_profile_read", "bloomhip_profile_reset", "bloomhip_trim", "bloomhip_host_positions",
     "bloomhip_gen_mt19937", "bloomhip_gen_glibc_rand", "bloomhip_gen_puts",
     "bloomhip_gen_workload", "bloomhip_set_batch_run", "bloomhip_set_run_meta",
-    "bloomhip_get_run_meta", "bloomhip_route_gets", "bloomhip_save", "bloomhip_load",
+    "bloomhip_get_run_meta", "bloomhip_route_gets", "bloomhip_route_gets_packed", "bloomhip_save", "bloomhip_load",
     "bloomhip_build_from_run_file", "bloomhip_compact", "bloomhip_clone",
 )
 
@@ -137,6 +137,7 @@ def _lib():
             "bloomhip_get_run_meta": (I, [P, P, SZ, ctypes.POINTER(SZ),
                                           ctypes.POINTER(ctypes.c_int32)]),
             "bloomhip_route_gets": (I, [ctypes.POINTER(P), I, P, SZ, SZ, I, P, P, P, I, P]),
+            "bloomhip_route_gets_packed": (I, [ctypes.POINTER(P), I, P, SZ, SZ, I, P, P, I, P]),
             "bloomhip_compact": (I, [ctypes.POINTER(P), P, I, I, I, P, ctypes.POINTER(SZ), I, P,
                                      I, P]),
             "bloomhip_save": (I, [P, ctypes.c_char_p]),
@@ -468,6 +469,46 @@ def route_gets(runs: Sequence[BloomFilter], keys, n: int | None = None, stride: 
                                       outs[2][0], out_dev, _stream_ptr(stream)),
            "bloomhip_route_gets")
     return cand, first, page
+
+
+ROUTE_NONE = 0xFFFFFFFF   # BLOOMHIP_ROUTE_NONE: no candidate run
+ROUTE_PAGE_BITS = 28
+
+
+def route_gets_packed(runs: Sequence[BloomFilter], keys, n: int | None = None, stride: int = 4,
+                      cand=None, route=None, stream=None):
+    """Batched GET routing with the packed output (bloomhip_route_gets_packed):
+    runs newest first (at most 16).  Returns (cand [nruns, ceil(n/64)] uint64
+    packed, route uint32[n]) with route[i] = first << 28 | page, or
+    ROUTE_NONE; pass device tensors for both to keep them on the device."""
+    ptr, on_dev, keep = _keys_ptr(keys, stride)
+    n = _key_count(keep, stride, n)
+    nr = len(runs)
+    nw = (n + 63) // 64
+    if cand is None and route is None:
+        cand = np.zeros((nr, nw), dtype=np.uint64)
+        route = np.empty(n, dtype=np.uint32)
+    need = ((nr * nw * 8, 8, "cand"), (n * 4, 4, "route"))
+    outs = [_out_ptr(x, *nd) if x is not None else (None, None, None)
+            for x, nd in zip((cand, route), need)]
+    devs = {o[1] for o in outs if o[0] is not None}
+    if len(devs) > 1:
+        raise ValueError("route_gets_packed outputs must be all host or all device buffers")
+    out_dev = devs.pop() if devs else 0
+    arr = (ctypes.c_void_p * nr)(*[r.handle.value for r in runs])
+    _check(_lib().bloomhip_route_gets_packed(arr, nr, ptr, n, stride, on_dev, outs[0][0], outs[1][0],
+                                             out_dev, _stream_ptr(stream)),
+           "bloomhip_route_gets_packed")
+    return cand, route
+
+
+def unpack_route(route):
+    """(first, page) int32 arrays from a packed route array, -1 where none."""
+    r = np.asarray(route, dtype=np.uint32)
+    none = r == ROUTE_NONE
+    first = np.where(none, -1, (r >> ROUTE_PAGE_BITS).astype(np.int32)).astype(np.int32)
+    page = np.where(none, -1, (r & ((1 << ROUTE_PAGE_BITS) - 1)).astype(np.int32)).astype(np.int32)
+    return first, page
 
 
 def compact(runs, drop_tombstones: bool = False, filter: BloomFilter | None = None,

@@ -31,6 +31,16 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// One spin-wait step of the host polls below: the x86 pause hint, the
+// AArch64 yield hint, nothing elsewhere.
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#elif defined(__aarch64__)
+    __builtin_arm_yield();
+#endif
+}
+
 int fail_hip(hipError_t e, const char *what) {
     g_last_error = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
     if (e == hipErrorOutOfMemory) return BLOOMHIP_ENOMEM;
@@ -771,7 +781,7 @@ int effective_probe_strategy(const bloomhip_filter *f, int owner_strategy) {
 // it was.
 struct FusedRoute {
     const RouteTable *rt;
-    int32_t *first, *page;
+    RouteOut out;
     bool routed;
 };
 
@@ -832,7 +842,7 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
         // tiles (two per CU) route faster (the f = 10 tree: 0.351 against
         // 0.387 ms, while its plain probe gains from super-tiles)
         if (fuse && ws.tile_keys == kSuperTileKeys &&
-            2 * ((size_t)route->rt->total_fences * 4 + 3 * kSuperTileKeys + 1024) > kLdsBitmapBytes)
+            2 * combine_route_lds_bytes(route->rt->total_fences, kSuperTileKeys) > kLdsBitmapBytes)
             ws.tile_keys = 0;
         const LockedWorkspace w(f0->device, s);
         int rc = partition_buffers(w.get(), n, s, &ws);
@@ -841,7 +851,7 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
         if (rc) return rc;
         hipError_t e = timed(f0, fuse ? SLOT_PROBE_STACK_ROUTE : SLOT_PROBE_STACK, s, [&] {
             return fuse ? launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s,
-                                               route->rt, route->first, route->page)
+                                               route->rt, route->out)
                         : launch_probe_stacked(ks, filters[h]->mp, st, ws, w->res, w->slots, dout, nw, s);
         });
         if (fuse && e == hipSuccess) route->routed = true;
@@ -958,11 +968,16 @@ int bloomhip_test_batch(const bloomhip_filter *const *filters, int nf, const voi
     return BLOOMHIP_OK;
 }
 
-int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const void *keys, size_t n,
-                        size_t stride_bytes, int keys_on_device, uint64_t *cand_packed,
-                        int32_t *first_run, int32_t *page, int out_on_device, void *stream) {
+namespace {
+
+// bloomhip_route_gets and bloomhip_route_gets_packed: the candidate rows and
+// either first / page or their packed form (each output optional).
+int route_impl(const bloomhip_filter *const *runs, int nruns, const void *keys, size_t n,
+               size_t stride_bytes, int keys_on_device, uint64_t *cand_packed, int32_t *first_run,
+               int32_t *page, uint32_t *packed, int out_on_device, void *stream) {
     g_last_error.clear();
     if (!runs || nruns <= 0 || nruns > kMaxRouteRuns) return BLOOMHIP_EINVAL;
+    if (packed && nruns > kRoutePackedMaxRuns) return BLOOMHIP_EINVAL;
     for (int j = 0; j < nruns; j++)
         if (!runs[j] || runs[j]->device != runs[0]->device) return BLOOMHIP_EINVAL;
     if (n == 0) return BLOOMHIP_OK;
@@ -998,30 +1013,50 @@ int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const voi
         HIP_TRY(grow(&f0->d_out_stage, &f0->out_stage_bytes, cand_bytes));
         dcand = reinterpret_cast<uint64_t *>(f0->d_out_stage);
     }
-    int32_t *dfirst = out_on_device ? first_run : nullptr;
-    int32_t *dpage = out_on_device ? page : nullptr;
-    if (!out_on_device && (first_run || page)) {
+    RouteOut ro{};
+    if (out_on_device) {
+        ro = RouteOut{first_run, page, packed};
+    } else if (first_run || page || packed) {
         HIP_TRY(grow(&f0->d_route_stage, &f0->route_stage_bytes, n * 8));
-        dfirst = first_run ? reinterpret_cast<int32_t *>(f0->d_route_stage) : nullptr;
-        dpage = page ? reinterpret_cast<int32_t *>(f0->d_route_stage) + n : nullptr;
+        int32_t *stage = reinterpret_cast<int32_t *>(f0->d_route_stage);
+        ro.first = first_run ? stage : nullptr;
+        ro.page = page ? stage + n : nullptr;
+        ro.packed = packed ? reinterpret_cast<uint32_t *>(stage) : nullptr;
     }
-    FusedRoute fr{&t, dfirst, dpage, false};
+    FusedRoute fr{&t, ro, false};
     rc = probe_rows(f0, runs, nruns, ks, n, dcand, s, &fr);
     if (rc) return rc;
     if (!fr.routed) {  // the filters were probed apart: route over their rows
-        hipError_t e = timed(f0, SLOT_ROUTE, s,
-                             [&] { return launch_route(ks, t, dcand, nw, dfirst, dpage, s); });
+        hipError_t e = timed(f0, SLOT_ROUTE, s, [&] { return launch_route(ks, t, dcand, nw, ro, s); });
         if (e != hipSuccess) return fail_hip(e, "k_route launch");
     }
     if (!out_on_device) {
         if (cand_packed)
             HIP_TRY(hipMemcpyAsync(cand_packed, dcand, cand_bytes, hipMemcpyDeviceToHost, s));
         if (first_run)
-            HIP_TRY(hipMemcpyAsync(first_run, dfirst, n * 4, hipMemcpyDeviceToHost, s));
-        if (page) HIP_TRY(hipMemcpyAsync(page, dpage, n * 4, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(first_run, ro.first, n * 4, hipMemcpyDeviceToHost, s));
+        if (page) HIP_TRY(hipMemcpyAsync(page, ro.page, n * 4, hipMemcpyDeviceToHost, s));
+        if (packed) HIP_TRY(hipMemcpyAsync(packed, ro.packed, n * 4, hipMemcpyDeviceToHost, s));
     }
     if (!keys_on_device || !out_on_device) HIP_TRY(hipStreamSynchronize(s));
     return BLOOMHIP_OK;
+}
+
+}  // namespace
+
+int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const void *keys, size_t n,
+                        size_t stride_bytes, int keys_on_device, uint64_t *cand_packed,
+                        int32_t *first_run, int32_t *page, int out_on_device, void *stream) {
+    return route_impl(runs, nruns, keys, n, stride_bytes, keys_on_device, cand_packed, first_run, page,
+                      nullptr, out_on_device, stream);
+}
+
+int bloomhip_route_gets_packed(const bloomhip_filter *const *runs, int nruns, const void *keys,
+                               size_t n, size_t stride_bytes, int keys_on_device,
+                               uint64_t *cand_packed, uint32_t *route, int out_on_device,
+                               void *stream) {
+    return route_impl(runs, nruns, keys, n, stride_bytes, keys_on_device, cand_packed, nullptr,
+                      nullptr, route, out_on_device, stream);
 }
 
 int bloomhip_set(bloomhip_filter *f, int32_t key) {
@@ -1065,7 +1100,7 @@ int bloomhip_is_set(const bloomhip_filter *fc, int32_t key, int *hit_out) {
     constexpr std::chrono::microseconds kIsSetSpin{1000};
     volatile uint32_t *hv = reinterpret_cast<volatile uint32_t *>(f->h_hit);
     const auto t0 = std::chrono::steady_clock::now();
-    while (*hv == 2u && std::chrono::steady_clock::now() - t0 < kIsSetSpin) __builtin_ia32_pause();
+    while (*hv == 2u && std::chrono::steady_clock::now() - t0 < kIsSetSpin) cpu_relax();
     // (A hipStreamQuery after a successful spin, to report a kernel fault at
     // once, made the call 12.0 us median against 8.7 without it, bench
     // scalar_is_set; a fault is sticky and surfaces at the next synchronising
@@ -1332,7 +1367,7 @@ int bloomhip_compact(const void *const *runs, const size_t *nentries, int nruns,
             constexpr std::chrono::microseconds kKeptSpin{2000};
             const auto t0 = std::chrono::steady_clock::now();
             while (*hk == kKeptPending && std::chrono::steady_clock::now() - t0 < kKeptSpin)
-                __builtin_ia32_pause();
+                cpu_relax();
             if (*hk == kKeptPending) HIP_TRY(hipStreamSynchronize(s));
             kept = *hk;
             if (kept > total) return fail_hip(hipErrorUnknown, "k-way compaction count not visible");

@@ -269,17 +269,8 @@ __device__ __forceinline__ void bin_entry(uint64_t raw, const ModParams &mp, con
 // atomics; 3 + the scan and the run table; 4 + the scatter; 5 + the packing,
 // without the sorted tile's stores.  A stage's unconsumed results go to one
 // store that only an impossible value takes.
-//
-// HC > 1: HC copies of the histogram, counter (bin b, copy c) at word
-// b * HC + c, lane l counting in copy c = l % HC.  A wave's 32-lane half
-// then spreads its rank atomics and offset reads over the banks by copy
-// class (bank 4 (b mod 8) + c at HC = 4: 8 lanes over 8 banks instead of
-// 32 over 32, a smaller expected worst bank); the scan runs over the
-// copies bin-major, so bin b's run of the tile is still one contiguous
-// range (the concatenation of its copies' ranks).  One bin per scanning
-// thread (nbins < TB).
 template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4,
-          int ABL = 0, int HC = 1>
+          int ABL = 0>
 __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                                                        uint64_t *__restrict__ pos_out,
                                                        uint32_t *__restrict__ runs, SegMap sm,
@@ -287,22 +278,20 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
     constexpr int kTileKeys = TB * kPartKPT;
     constexpr int kTilePos = 3 * kTileKeys;
     constexpr int kMaxB = MAXB ? MAXB : TB >= 1024 ? (int)kPartMaxBinsBig : (int)kPartMaxBins;
-    constexpr int kScanPer = HC > 1 ? HC : (kMaxB + 1 + TB - 1) / TB;  // scan entries per thread, at most
+    constexpr int kScanPer = (kMaxB + 1 + TB - 1) / TB;  // scan entries per thread, at most
     static_assert(4 * kTilePos <= (1 << 17) && kTilePos < (1 << 16) &&
-                      ((uint64_t)((kMaxB + 1) * HC - 2) << kBinShift) < (1ull << 32),
+                      ((uint64_t)(kMaxB - 1) << kBinShift) < (1ull << 32),
                   "packed rank fields (bin nbins, never incremented, may wrap to 0)");
-    static_assert(HC == 1 || (HC == 4 && kMaxB < TB), "copies: one bin per scanning thread");
     // static LDS even for the 96 KiB of an 8192-key tile (gfx950 takes it);
     // dynamic LDS or a pointer to it made the compiler spill registers here
     __shared__ __attribute__((aligned(16))) uint32_t s_sorted[kTilePos];
-    __shared__ __attribute__((aligned(16))) uint32_t s_hist[(kMaxB + 1) * HC];
+    __shared__ uint32_t s_hist[kMaxB + 1];
     __shared__ uint32_t s_wsum[TB / 64];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int nb = (int)sm.nbins;
-    const int per = HC > 1 ? HC : (nb + 1 + TB - 1) / TB;  // this launch's scan entries per thread
-    const uint32_t hc = (uint32_t)lane & (HC - 1);          // this lane's histogram copy
+    const int per = (nb + 1 + TB - 1) / TB;  // this launch's scan entries per thread
     int32_t kcur[kPartKPT], knext[kPartKPT];
 
     // One tile.  FULL (every tile but a short last one) makes the key count a
@@ -316,7 +305,7 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
         const int tile_keys = FULL ? (int)kTileKeys : (int)min((size_t)kTileKeys, ks.n - tile0);
         auto live = [&](int j) { return FULL || kPartKPT * tid + j < tile_keys; };
 #pragma clang loop unroll(disable) vectorize(disable)
-        for (int b = tid; b < (nb + 1) * HC; b += TB) s_hist[b] = (uint32_t)b << kBinShift;
+        for (int b = tid; b <= nb; b += TB) s_hist[b] = (uint32_t)b << kBinShift;
         lds_barrier();  // also: the previous tile's s_sorted reads are done
 
         // 1. positions -> (segment, rank in segment) and the entry; the ranks
@@ -335,7 +324,7 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                     bin_entry<MK, MINW>(raw, mp, sm, b, e);
                     ent[3 * j + h] = e;
                     if constexpr (ABL == 1) br[3 * j + h] = b;
-                    else br[3 * j + h] = atomicAdd(&s_hist[HC > 1 ? b * HC + hc : b], 4u);
+                    else br[3 * j + h] = atomicAdd(&s_hist[b], 4u);
                 }
             } else {
 #pragma unroll
@@ -360,53 +349,9 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
         //    receives the tile total); thread t owns [t*per, t*per + per).
         //    Waves that own no bin (C2: waves 5-7 of 8) skip it: nobody
         //    reads their wave sums, which come after every live bin.
-        const bool scan_wave = wave * 64 * (HC > 1 ? 1 : per) <= nb;  // uniform per wave
+        const bool scan_wave = wave * 64 * per <= nb;  // uniform per wave
         uint32_t local[kScanPer];  // 4 * count of bin b
         uint32_t tsum = 0, incl = 0;
-        if constexpr (HC > 1) {
-            // thread t owns bin t's HC counters (one 16-B read; read again
-            // after the barrier rather than kept in registers)
-            (void)local;
-            // counter b * HC + c holds its (b * HC + c) << kBinShift bias
-            // plus 4 * count: the four biases differ by 1 << kBinShift
-            auto counts = [&](const uint4 &c4, uint32_t &x, uint32_t &y, uint32_t &z) {
-                const uint32_t q0 = (uint32_t)(tid * HC) << kBinShift;
-                x = c4.x - q0;
-                y = c4.y - q0 - (1u << kBinShift);
-                z = c4.z - q0 - (2u << kBinShift);
-                return c4.w - q0 - (3u << kBinShift);
-            };
-            if (scan_wave) {
-                if (tid <= nb) {
-                    uint32_t x, y, z;
-                    const uint32_t w = counts(*reinterpret_cast<const uint4 *>(s_hist + tid * HC), x, y, z);
-                    tsum = x + y + z + w;
-                }
-                incl = wave_incl_scan(tsum);
-                if (lane == 63) s_wsum[wave] = incl;
-            }
-            lds_barrier();
-            if (scan_wave) {
-                uint32_t run = incl - tsum;
-                for (int w = 0; w < wave; w++) run += s_wsum[w];
-                if (tid <= nb) {
-                    const uint32_t q0 = (uint32_t)(tid * HC) << kBinShift;
-                    uint32_t x, y, z;
-                    (void)counts(*reinterpret_cast<const uint4 *>(s_hist + tid * HC), x, y, z);
-                    uint4 o;
-                    o.x = run - q0;
-                    o.y = run + x - q0 - (1u << kBinShift);
-                    o.z = run + x + y - q0 - (2u << kBinShift);
-                    o.w = run + x + y + z - q0 - (3u << kBinShift);
-                    *reinterpret_cast<uint4 *>(s_hist + tid * HC) = o;
-                    const uint32_t pk = (run >> 2) | (((run + tsum) >> 2) << 16);
-                    if (tid < nb) {
-                        if constexpr (COLS) runs[(size_t)tid * ntiles + tile] = pk;
-                        else runs[tile * (size_t)nb + tid] = pk;
-                    }
-                }
-            }
-        } else {
         if (scan_wave) {
 #pragma unroll
             for (int q = 0; q < kScanPer; q++) {
@@ -439,7 +384,6 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                     run += local[q];
                 }
             }
-        }
         }
         lds_barrier();
         if (next < ntiles) load_tile_keys<LAYOUT, TB>(ks, next, tid, knext);
@@ -1632,7 +1576,8 @@ template <int TILE_KEYS, int BLOCK, int LAYOUT>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) k_probe_combine_route(
     const uint8_t *__restrict__ res, const uint16_t *__restrict__ slots, KeySpan ks,
     uint64_t *__restrict__ out, size_t nw, StackTable rows, RouteTable rt,
-    int32_t *__restrict__ first, int32_t *__restrict__ page, size_t ntiles) {
+    int32_t *__restrict__ first, int32_t *__restrict__ page, uint32_t *__restrict__ packed,
+    size_t ntiles) {
     constexpr int kTilePos = 3 * TILE_KEYS;
     constexpr int kPasses = TILE_KEYS / (BLOCK * kCombineKeys);  // super-tiles: two
     static_assert(kPasses * BLOCK * kCombineKeys == TILE_KEYS, "8 keys per thread and pass");
@@ -1686,7 +1631,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
         }
     }
     const int kt = kCombineKeys * (int)threadIdx.x;  // this thread's first key in a tile's pass
-    const bool vec_out = ((reinterpret_cast<uintptr_t>(first) | reinterpret_cast<uintptr_t>(page)) & 15) == 0;
+    const bool vec_out = ((reinterpret_cast<uintptr_t>(first) | reinterpret_cast<uintptr_t>(page) |
+                           reinterpret_cast<uintptr_t>(packed)) & 15) == 0;
     for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t tile0 = tile * TILE_KEYS;
         const int tile_keys = (int)min((size_t)TILE_KEYS, ks.n - tile0);
@@ -1811,7 +1757,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
                 pg[i] = fr[i] >= 0 ? lo_[u] - 1 : -1;
             }
         }
-        // first / page of the live keys
+        // first / page (or their packed form) of the live keys
         if (vec_out && tile_keys == TILE_KEYS) {
             int4 *f4 = reinterpret_cast<int4 *>(first + tile0 + k0);
             int4 *p4 = reinterpret_cast<int4 *>(page + tile0 + k0);
@@ -1823,12 +1769,20 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
                 p4[0] = make_int4(pg[0], pg[1], pg[2], pg[3]);
                 p4[1] = make_int4(pg[4], pg[5], pg[6], pg[7]);
             }
+            if (packed) {
+                uint4 *q4 = reinterpret_cast<uint4 *>(packed + tile0 + k0);
+                q4[0] = make_uint4(route_pack(fr[0], pg[0]), route_pack(fr[1], pg[1]),
+                                   route_pack(fr[2], pg[2]), route_pack(fr[3], pg[3]));
+                q4[1] = make_uint4(route_pack(fr[4], pg[4]), route_pack(fr[5], pg[5]),
+                                   route_pack(fr[6], pg[6]), route_pack(fr[7], pg[7]));
+            }
         } else {
 #pragma unroll
             for (int i = 0; i < kCombineKeys; i++) {
                 if (k0 + i < tile_keys) {
                     if (first) first[tile0 + k0 + i] = fr[i];
                     if (page) page[tile0 + k0 + i] = pg[i];
+                    if (packed) packed[tile0 + k0 + i] = route_pack(fr[i], pg[i]);
                 }
             }
         }

@@ -42,6 +42,28 @@ constexpr int kMaxRouteRuns = 64;
 // and a binary search in global memory took 0.59 ms for its 16.8M GETs.
 // Dynamic LDS within 64 KiB needs no opt-in.
 constexpr size_t kRouteLdsFenceBytesMax = 60u << 10;
+// Packed route output (bloomhip_route_gets_packed): one u32 per GET, the
+// newest candidate run in bits 28-31 and its page in bits 0-27, or
+// kRouteNone; half the bytes of the two int32 arrays first / page.
+constexpr uint32_t kRouteNone = 0xFFFFFFFFu;
+constexpr int kRoutePackedMaxRuns = 16;
+constexpr uint32_t kRoutePageBits = 28;
+__host__ __device__ __forceinline__ uint32_t route_pack(int32_t run, int32_t page) {
+    return run >= 0 ? ((uint32_t)run << kRoutePageBits) | (uint32_t)page : kRouteNone;
+}
+// The route outputs of a routing call, each optional (null to skip).
+struct RouteOut {
+    int32_t *first;
+    int32_t *page;
+    uint32_t *packed;
+};
+// LDS of one workgroup of the combine with routing fused in
+// (k_probe_combine_route): the runs' fences (dynamic), the tile's result
+// bytes (3 per key, static) and the per-run tables (static, < 1 KiB).  The
+// launch and probe_stacks' tile choice both size from this one helper.
+inline size_t combine_route_lds_bytes(uint32_t total_fences, size_t tile_keys) {
+    return (size_t)total_fences * 4 + 3 * tile_keys + 1024;
+}
 
 // Run metadata on the device: meta[0] = max key, meta[1 .. nfences] = the
 // fence pointers, ascending (a run is written sorted).
@@ -308,7 +330,7 @@ hipError_t launch_run_meta_sorted(const KeySpan &keys, int32_t *meta, hipStream_
 // Applies the range checks to the probe rows `cand` in place and writes the
 // newest candidate run and its page index per key (first/page may be null).
 hipError_t launch_route(const KeySpan &keys, const RouteTable &t, uint64_t *cand, size_t nw,
-                        int32_t *first, int32_t *page, hipStream_t stream);
+                        const RouteOut &ro, hipStream_t stream);
 // Partitioned probe of one filter (nbins as plan_segments): bin the
 // keys' positions by segment (recording each position's sorted slot), test
 // each segment in LDS writing one result byte per sorted entry, then AND each
@@ -320,12 +342,11 @@ hipError_t launch_route(const KeySpan &keys, const RouteTable &t, uint64_t *cand
 // rt (GET routing fused into the combine, k_probe_combine_route): every run
 // of the routing call is a member (rt->nruns == st.nf, st.row a permutation)
 // and their fences fit kRouteLdsFenceBytesMax; out then gets the range-checked
-// candidate rows and first / page (either may be null) what k_route writes.
+// candidate rows and the route outputs (each may be null) what k_route writes.
 hipError_t launch_probe_stacked(const KeySpan &keys, const ModParams &mp_max, const StackTable &st,
                                 const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
                                 uint64_t *out, size_t nw, hipStream_t stream,
-                                const RouteTable *rt = nullptr, int32_t *first = nullptr,
-                                int32_t *page = nullptr);
+                                const RouteTable *rt = nullptr, const RouteOut &ro = RouteOut{});
 hipError_t launch_probe_partitioned(const KeySpan &keys, const ModParams &mp, const uint32_t *words,
                                     const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
                                     uint64_t *out, hipStream_t stream);

@@ -340,7 +340,8 @@ template <int LAYOUT, bool LDS_FENCES, int NR>
 __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
                                                       uint64_t *__restrict__ cand, size_t nw,
                                                       int32_t *__restrict__ first,
-                                                      int32_t *__restrict__ page) {
+                                                      int32_t *__restrict__ page,
+                                                      uint32_t *__restrict__ packed) {
     extern __shared__ int32_t s_fences[];
     __shared__ int32_t s_lo[kMaxRouteRuns], s_hi[kMaxRouteRuns];
     __shared__ uint32_t s_nf[kMaxRouteRuns], s_off[kMaxRouteRuns];
@@ -440,6 +441,7 @@ __global__ void __launch_bounds__(kRouteBlock) k_route(KeySpan ks, RouteTable t,
         if (valid) {
             if (first) first[i] = fr;
             if (page) page[i] = pg;
+            if (packed) packed[i] = route_pack(fr, pg);
         }
     };
     int32_t ka = load_key_at(w);
@@ -650,11 +652,17 @@ bool plan_stack(uint64_t m_max, uint64_t gcd_m, uint64_t m_min, int nf, int ncu,
         if (a != b) return a;
         return a ? w > best_w : w < best_w;
     };
+    // Only w that are multiples of 128 bits count, so below s = 7 g steps by
+    // 2^(7 - s); and g falls, so the scan of an s ends where w leaves more
+    // than kPartMaxBinsBig segments (a few hundred candidates per call, not
+    // the ~wmax a unit step visits)
     for (uint32_t s = 1; s < 32 && (1ull << s) <= wmax; s++) {
         if (m_max % (1ull << s)) break;  // larger s cannot divide either
-        for (uint64_t g = wmax >> s; g >= 1; g--) {
+        const uint64_t gstep = s < 7 ? 1ull << (7 - s) : 1ull;
+        for (uint64_t g = (wmax >> s) / gstep * gstep; g >= 1; g -= gstep) {
             const uint64_t w = g << s;
-            if (w % 128 || m_max % w || w > m_min || m_max / w > kPartMaxBinsBig) continue;
+            if (m_max / w > kPartMaxBinsBig) break;  // and for every smaller g
+            if (w % 128 || m_max % w || w > m_min) continue;
             if (!(better(w) || (w == best_w && s > best_s))) continue;
             uint32_t magic = 0;
             if (!seg_magic((uint32_t)g, m_max >> s, &magic)) continue;
@@ -879,7 +887,8 @@ hipError_t launch_run_meta(const KeySpan &ks, int32_t *meta, hipStream_t stream)
 }
 
 hipError_t launch_route(const KeySpan &ks, const RouteTable &t, uint64_t *cand, size_t nw,
-                        int32_t *first, int32_t *page, hipStream_t stream) {
+                        const RouteOut &ro, hipStream_t stream) {
+    if (ro.packed && t.nruns > kRoutePackedMaxRuns) return hipErrorInvalidValue;
     if (nw == 0) return hipSuccess;
     const size_t lds = (size_t)t.total_fences * 4;
     // Fences from LDS beat L2 reads.  The grid is what fits on the chip at
@@ -891,7 +900,7 @@ hipError_t launch_route(const KeySpan &ks, const RouteTable &t, uint64_t *cand, 
     per_cu = per_cu < 1 ? 1 : per_cu > 8 ? 8 : per_cu;  // 8 x 256 threads = 32 waves per CU
     const unsigned grid = grid_for(nw, kRouteBlock / 64, (unsigned)(device_cu_count() * per_cu));
 #define ROUTE_LAUNCH(L, F, R) \
-    k_route<L, F, R><<<grid, kRouteBlock, F ? lds : 0, stream>>>(ks, t, cand, nw, first, page)
+    k_route<L, F, R><<<grid, kRouteBlock, F ? lds : 0, stream>>>(ks, t, cand, nw, ro.first, ro.page, ro.packed)
 #define ROUTE_NR(L, F)                                                          \
     switch (t.nruns) {                                                          \
         case 1: ROUTE_LAUNCH(L, F, 1); break;                                   \

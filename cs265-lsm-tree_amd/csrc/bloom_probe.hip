@@ -46,9 +46,10 @@ hipError_t launch_probe_partitioned(const KeySpan &ks, const ModParams &mp, cons
 // in LDS; else hipErrorInvalidValue before anything is launched.
 hipError_t launch_combine_route(const PartitionWorkspace &ws, const uint8_t *res,
                                 const uint16_t *slots, const KeySpan &ks, uint64_t *out, size_t nw,
-                                const StackTable &rows, const RouteTable &rt, int32_t *first,
-                                int32_t *page, hipStream_t stream) {
+                                const StackTable &rows, const RouteTable &rt, const RouteOut &ro,
+                                hipStream_t stream) {
     if (rt.nruns != rows.nf || (size_t)rt.total_fences * 4 > kRouteLdsFenceBytesMax) return hipErrorInvalidValue;
+    if (ro.packed && rt.nruns > kRoutePackedMaxRuns) return hipErrorInvalidValue;
     unsigned seen = 0;
     for (int j = 0; j < rows.nf; j++) {
         if (rows.row[j] < 0 || rows.row[j] >= rows.nf) return hipErrorInvalidValue;
@@ -61,17 +62,17 @@ hipError_t launch_combine_route(const PartitionWorkspace &ws, const uint8_t *res
     // while two copies of the fences and the tile's result bytes fit the
     // LDS, else one (a second round of workgroups would start only when the
     // first has walked all of its tiles)
-    const size_t per_wg = lds + 3 * (size_t)tile_keys_of(ws) + 1024;
+    const size_t per_wg = combine_route_lds_bytes(rt.total_fences, tile_keys_of(ws));
     const size_t cap = (size_t)device_cu_count() * (2 * per_wg <= kLdsBitmapBytes ? 2 : 1);
     const unsigned grid = (unsigned)(ws.ntiles < cap ? ws.ntiles : cap);
 #define COMBINE_ROUTE(TK, L)                                                                      \
     k_probe_combine_route<TK, TK / kCombineKeys, L><<<grid, TK / kCombineKeys, lds, stream>>>(    \
-        res, slots, ks, out, nw, rows, rt, first, page, ws.ntiles)
+        res, slots, ks, out, nw, rows, rt, ro.first, ro.page, ro.packed, ws.ntiles)
     const bool big = tile_keys_of(ws) == 2 * kPartTileKeys, super = tile_keys_of(ws) == kSuperTileKeys;
     constexpr int kSuper = (int)kSuperTileKeys;
 #define COMBINE_ROUTE_SUPER(L)                                                                    \
     k_probe_combine_route<kSuper, 1024, L><<<grid, 1024, lds, stream>>>(                          \
-        res, slots, ks, out, nw, rows, rt, first, page, ws.ntiles)
+        res, slots, ks, out, nw, rows, rt, ro.first, ro.page, ro.packed, ws.ntiles)
     if (ks.layout == KEYS_PACKED) {
         if (super) COMBINE_ROUTE_SUPER(KEYS_PACKED);
         else if (big) COMBINE_ROUTE(kBig, KEYS_PACKED); else COMBINE_ROUTE(kSmall, KEYS_PACKED);
@@ -87,12 +88,12 @@ hipError_t launch_combine_route(const PartitionWorkspace &ws, const uint8_t *res
 hipError_t launch_probe_stacked(const KeySpan &ks, const ModParams &mp_max, const StackTable &st,
                                 const PartitionWorkspace &ws, uint8_t *res, uint16_t *slots,
                                 uint64_t *out, size_t nw, hipStream_t stream, const RouteTable *rt,
-                                int32_t *first, int32_t *page) {
+                                const RouteOut &ro) {
     if (ks.n == 0) return hipSuccess;
     if (rt && (rt->nruns != st.nf || (size_t)rt->total_fences * 4 > kRouteLdsFenceBytesMax))
         return hipErrorInvalidValue;
     auto combine = [&]() {
-        return rt ? launch_combine_route(ws, res, slots, ks, out, nw, st, *rt, first, page, stream)
+        return rt ? launch_combine_route(ws, res, slots, ks, out, nw, st, *rt, ro, stream)
                   : launch_combine(ws, res, slots, ks.n, out, nw, st, stream);
     };
     if (st.ladder) {  // plan_ladder's geometry

@@ -306,22 +306,6 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     }
         UB_ABL(0) UB_ABL(1) UB_ABL(2) UB_ABL(3) UB_ABL(4) UB_ABL(5)
 #undef UB_ABL
-        // 5110 + ABL: the same with four histogram copies (k_part_bin's HC = 4,
-        // capacity 256 bins so three workgroups still fit a CU)
-#define UB_HC(A)                                                                                  \
-    case 5110 + A: {                                                                             \
-        SegMap sm{};                                                                             \
-        if (pass1_plan(mp, ws, false, &sm) != kModLadder0R || ws.tile_keys != 4096 ||           \
-            ws.nbins > 256 || !runs_as_columns(ws))                                              \
-            return -22;                                                                          \
-        const unsigned g = (unsigned)std::min<size_t>(ws.ntiles, (size_t)device_cu_count() * 3); \
-        k_part_bin<KEYS_PACKED, false, true, 512, kModLadder0R, 256, 6, A, 4>                    \
-            <<<g, 512, 0, s>>>(ks, mp, ws.pos, ws.run_starts, sm, ws.ntiles, nullptr);           \
-        e = hipGetLastError();                                                                   \
-        break;                                                                                   \
-    }
-        UB_HC(0) UB_HC(2) UB_HC(3) UB_HC(5)
-#undef UB_HC
         default: return -22;
     }
     return e == hipSuccess ? 0 : -5;

@@ -160,6 +160,18 @@ int bloomhip_route_gets(const bloomhip_filter *const *runs, int nruns, const voi
                         size_t n, size_t stride_bytes, int keys_on_device,
                         uint64_t *cand_packed, int32_t *first_run, int32_t *page,
                         int out_on_device, void *stream);
+/* The same routing with first_run and page packed into one u32 per GET, half
+ * the output bytes of the two int32 arrays (the GET's whole answer for
+ * Run::get, src/run.cpp:93-99, in one word):
+ *   route[i] = first_run[i] << 28 | page[i]   when key i has a candidate run,
+ *              BLOOMHIP_ROUTE_NONE            when it has none.
+ * nruns <= 16.  cand_packed as above; each output optional (NULL to skip). */
+#define BLOOMHIP_ROUTE_NONE 0xFFFFFFFFu
+#define BLOOMHIP_ROUTE_PAGE_BITS 28
+int bloomhip_route_gets_packed(const bloomhip_filter *const *runs, int nruns, const void *keys,
+                               size_t n, size_t stride_bytes, int keys_on_device,
+                               uint64_t *cand_packed, uint32_t *route, int out_on_device,
+                               void *stream);
 
 /* --- persistence beside the run -------------------------
  * The reference keeps a run's entries in an mmap'd file (src/run.cpp:34-72)

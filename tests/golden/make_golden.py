@@ -16,6 +16,8 @@ Two kinds of vectors live here, kept apart on purpose:
 Run:  python tests/golden/make_golden.py   (about a minute, ~6 GB RAM)
       python tests/golden/make_golden.py f10   (adds / refreshes only the
       f = 10 tree's pins in pins.json, leaving the rest as they are)
+      python tests/golden/make_golden.py route   (only the routing pins of
+      C3 and of the f = 10 tree, and the fan-in-4 compaction's pins)
 """
 import hashlib
 import json
@@ -88,13 +90,47 @@ def f10_pins(C):
     return out
 
 
+def route_pins(C, gets, levels):
+    """bo_route (src/run.cpp:93-99 over LSMTree::get's runs) of `gets` over
+    the level runs (distinct keys ascending, newest level first): SHA-256 of
+    the candidate rows, of first and page, and of their packed form
+    (first << 28 | page, 0xFFFFFFFF for none: bloomhip_route_gets_packed)."""
+    runs = []
+    for lvl, keys, m in levels:
+        fences, mk = C.run_meta(keys)
+        runs.append((C.build(m, keys), m, fences, mk))
+    cand, first, page = C.route(runs, gets)
+    packed = np.where(first < 0, np.uint32(0xFFFFFFFF),
+                      (first.astype(np.uint32) << np.uint32(28)) | page.astype(np.uint32))
+    return {"cand_sha256": sha(cand), "first_sha256": sha(first), "page_sha256": sha(page),
+            "route_sha256": sha(packed.astype(np.uint32)),
+            "keys_with_candidate": int((first >= 0).sum())}
+
+
+def compact_pins(C):
+    """bo_compact (src/merge.cpp:17-35, newest wins, tombstones dropped) of
+    the fan-in-4 compaction (workloads.compaction_fanin) and the new run's
+    filter built over the merged keys (entry_t stride 8)."""
+    runs, m = W.compaction_fanin()
+    merged = C.compact(runs, drop_tombstones=True)
+    w = C.build(m, merged.reshape(-1), stride=8, n=merged.shape[0])
+    return {"m": m, "entries_in": int(sum(r.shape[0] for r in runs)),
+            "entries_out": int(merged.shape[0]), "merged_sha256": sha(merged),
+            "filter_sha256": sha(w)}
+
+
 def main():
     C = COracle()
-    if sys.argv[1:] == ["f10"]:
+    if sys.argv[1:] in (["f10"], ["route"]):
         path = os.path.join(HERE, "pins.json")
         with open(path) as f:
             pins = json.load(f)
-        pins["oracle"]["f10"] = f10_pins(C)
+        if sys.argv[1] == "f10":
+            pins["oracle"]["f10"] = f10_pins(C)
+        else:
+            pins["oracle"]["route_c3"] = route_pins(C, *W.c3_runs())
+            pins["oracle"]["f10"]["route"] = route_pins(C, *W.f10_runs())
+            pins["oracle"]["compact_fanin4"] = compact_pins(C)
         with open(path, "w") as f:
             json.dump(pins, f, indent=1)
         print("updated", path)
@@ -144,6 +180,9 @@ def main():
                    "popcount": C.popcount(w5)})
     oracle["c5"] = c5
     oracle["f10"] = f10_pins(C)
+    oracle["route_c3"] = route_pins(C, *W.c3_runs())
+    oracle["f10"]["route"] = route_pins(C, *W.f10_runs())
+    oracle["compact_fanin4"] = compact_pins(C)
 
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump({"source": "SURVEY.md §8a / §0 F4 (compiled reference)",

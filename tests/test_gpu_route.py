@@ -111,6 +111,20 @@ def routed_by(runs, call):
     return ("fused" if fused else "k_route"), out
 
 
+def packed_matches(runs, gets, wc, wf, wp, path=None, **kw):
+    """bloomhip_route_gets_packed against the oracle's rows, first and page
+    (route[i] = first << 28 | page, or ROUTE_NONE), and the path it took."""
+    p, (cand, route) = routed_by(runs, lambda: bh.route_gets_packed(runs, gets, **kw))
+    if path is not None:
+        assert p == path
+    want = np.where(wf < 0, np.uint32(bh.ROUTE_NONE),
+                    (wf.astype(np.uint32) << np.uint32(bh.ROUTE_PAGE_BITS)) | wp.astype(np.uint32))
+    assert np.array_equal(cand, wc) and np.array_equal(route, want)
+    f, pg = bh.unpack_route(route)
+    assert np.array_equal(f, wf) and np.array_equal(pg, wp)
+    return route
+
+
 @pytest.mark.parametrize("probe", [bh.PROBE_AUTO, bh.PROBE_GATHER, bh.PROBE_PARTITION,
                                    bh.PROBE_LDS], ids=["auto", "gather", "partition", "lds"])
 def test_route_matches_oracle(coracle, probe):
@@ -122,6 +136,7 @@ def test_route_matches_oracle(coracle, probe):
     assert np.array_equal(first, wf)
     assert np.array_equal(page, wp)
     assert (first >= 0).sum() > 0 and (page[first >= 0] >= 0).all()
+    packed_matches(runs, gets, wc, wf, wp)
 
 
 def test_route_skewed_and_duplicate_fences(coracle):
@@ -154,6 +169,7 @@ def test_route_skewed_and_duplicate_fences(coracle):
     wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     assert (page[first == 1] > 0).any()  # pages past the first in the skewed run
+    packed_matches(runs, gets, wc, wf, wp, path="k_route")
 
 
 def test_route_many_runs_and_missing_meta(coracle):
@@ -173,6 +189,10 @@ def test_route_many_runs_and_missing_meta(coracle):
     wc, wf, wp = coracle.route(orefs, gets)
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     assert not cand[12].any() and not cand[7].any()
+    # the packed form holds a run index in 4 bits: more than 16 runs refused
+    with pytest.raises(bh.BloomHipError):
+        bh.route_gets_packed(runs, gets)
+    packed_matches(runs[:16], gets, *coracle.route(orefs[:16], gets), path="k_route")
 
 
 def test_route_device_buffers_and_strides(coracle):
@@ -192,6 +212,13 @@ def test_route_device_buffers_and_strides(coracle):
     aos[:, 0] = gets
     c2, f2, p2 = bh.route_gets(runs, aos.reshape(-1), n=n, stride=8)
     assert np.array_equal(c2, wc) and np.array_equal(f2, wf) and np.array_equal(p2, wp)
+    dr = torch.empty(n, dtype=torch.int32, device="cuda")
+    dc.zero_()
+    bh.route_gets_packed(runs, torch.from_numpy(gets).cuda(), cand=dc, route=dr)
+    torch.cuda.synchronize()
+    f3, p3 = bh.unpack_route(dr.cpu().numpy().view(np.uint32))
+    assert np.array_equal(dc.cpu().numpy().view(np.uint64), wc)
+    assert np.array_equal(f3, wf) and np.array_equal(p3, wp)
 
 
 def test_route_c3_full(coracle, golden):
@@ -209,6 +236,10 @@ def test_route_c3_full(coracle, golden):
     assert path == "fused"  # the five levels are one ladder stack (the bench's route_c3)
     wc, wf, wp = coracle.route(orefs, gets)
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
+    route = packed_matches(runs, gets, wc, wf, wp, path="fused")  # the bench's route_c3 form
+    rc3 = golden["oracle"]["route_c3"]
+    assert hashlib.sha256(wc.tobytes()).hexdigest() == rc3["cand_sha256"]
+    assert hashlib.sha256(route.tobytes()).hexdigest() == rc3["route_sha256"]
     # filter bits are the pinned C3 probe results restricted by the range check
     probe = bh.test_batch(runs, gets)
     assert ((cand & ~probe) == 0).all()
@@ -233,6 +264,10 @@ def test_route_f10_full(coracle, golden):
     assert path == "fused"
     wc, wf, wp = coracle.route(orefs, gets)
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
+    route = packed_matches(runs, gets, wc, wf, wp, path="fused")  # the bench's f10 route form
+    rf = golden["oracle"]["f10"]["route"]
+    assert hashlib.sha256(wc.tobytes()).hexdigest() == rf["cand_sha256"]
+    assert hashlib.sha256(route.tobytes()).hexdigest() == rf["route_sha256"]
     probe = bh.test_batch(runs, gets)
     for lvl in range(len(levels)):
         assert hashlib.sha256(probe[lvl].tobytes()).hexdigest() == \
@@ -289,6 +324,20 @@ def test_route_fused_into_stacked_combine(coracle, layout):
     assert path == "fused"  # the kernel under test really ran
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     assert not cand[1].any() and (first >= 0).sum() > 1000
+    if layout == "packed":
+        packed_matches(runs, gets, wc, wf, wp, path="fused")
+    elif layout == "entry":
+        packed_matches(runs, aos.reshape(-1), wc, wf, wp, path="fused", n=gets.size, stride=8)
+    else:
+        dr = torch.empty(n, dtype=torch.int32, device="cuda")
+        dc.zero_()
+        path, _ = routed_by(runs, lambda: bh.route_gets_packed(runs, torch.from_numpy(gets).cuda(),
+                                                                cand=dc, route=dr))
+        torch.cuda.synchronize()
+        assert path == "fused"
+        f3, p3 = bh.unpack_route(dr.cpu().numpy().view(np.uint32))
+        assert np.array_equal(dc.cpu().numpy().view(np.uint64), wc)
+        assert np.array_equal(f3, wf) and np.array_equal(p3, wp)
 
 
 def test_route_fused_duplicate_fences_and_edges(coracle):
@@ -327,6 +376,7 @@ def test_route_fused_duplicate_fences_and_edges(coracle):
     wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     assert (first == 1).any() and (page[first == 2] > 0).any()
+    packed_matches(runs, gets, wc, wf, wp, path="fused")
 
 
 @pytest.mark.parametrize("n", [100_001, 16_385])
@@ -344,3 +394,4 @@ def test_route_fused_on_super_tiles(coracle, n):
     wc, wf, wp = coracle.route(oracle_runs(coracle, refs), gets)
     assert np.array_equal(cand, wc) and np.array_equal(first, wf) and np.array_equal(page, wp)
     assert (first >= 0).sum() > n // 4
+    packed_matches(runs, gets, wc, wf, wp, path="fused")

@@ -191,17 +191,9 @@ def p1_ablation(n=16_777_216, bpe=10.0, rounds=3, reps=50):
     print(json.dumps({"check": "ablation variant 5100 bitmap == product", "ok": bool(torch.equal(ref, words))}),
           flush=True)
     names = {5101: "hash + bin/entry", 5102: "+ rank atomics", 5103: "+ scan, run table",
-             5105: "+ scatter + packing (no stores)", 5100: "whole pass 1", 0: "product pass 1",
-             5112: "HC=4: + rank atomics", 5113: "HC=4: + scan", 5115: "HC=4: + scatter + packing",
-             5110: "HC=4: whole pass 1"}
+             5105: "+ scatter + packing (no stores)", 5100: "whole pass 1", 0: "product pass 1"}
     # (ABL 4, the scatter without the packing, is left out: nothing reads the
     # scattered image, so the compiler drops the scatter and the entries)
-    words.zero_()
-    if run(5110) == 0:
-        run(1)
-        torch.cuda.synchronize()
-        print(json.dumps({"check": "HC=4 variant 5110 bitmap == product", "ok": bool(torch.equal(ref, words))}),
-              flush=True)
     _prewarm(run, 0)
     res = {v: [] for v in names}
     for _ in range(rounds):
