@@ -1272,7 +1272,85 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         }
     };
 
-    if constexpr (WALK == 1 || WALK == 2) {
+    if constexpr (WALK >= 4) {
+        // WALK 1 / 3 / 2's walks for builds (round 6: WALK 4 / 5 / 6),
+        // restated for fewer instructions per step: unrolled over two
+        // register sets (the old loops copy their carried state at the
+        // back-edge: seven moves a step), the vector and run-bound loads
+        // addressed from uniform bases by 32-bit byte offsets (the sorted
+        // tiles span < 4 GiB: the launchers check), so a step forms a load
+        // address in two instructions instead of eight 64-bit ones, and a
+        // run's end kept in vectors (the step test multiplies nothing).
+        // Lanes past the last tile hold an empty run (r = 0).  NV vectors
+        // per lane and step (WALK 5: two, for super-tiles' ~20-entry runs);
+        // REDIR (WALK 5, 6: short runs): a lane whose vector lies past the
+        // run's end loads the group's first vector instead (WALK 2's note).
+        // Launched: WALK 4 (C2, C5).  WALK 5 against WALK 3 on C4's
+        // super-tiles: 806 against 796 us (profiles/r06/rejected/walk5_c4/).
+        static_assert(!PROBE, "builds");
+        constexpr int NV = WALK == 5 ? 2 : 1;
+        constexpr bool REDIR = WALK >= 5;
+        constexpr int kGroupsPerWave = 64 / G;
+        const int Q = kGroupsPerWave * (BLOCK / 64);
+        constexpr uint32_t kVecShift = __builtin_ctz((unsigned)TILE_KEYS / 2);  // vectors per tile, log2
+        const char *pos_b = reinterpret_cast<const char *>(pos);
+        const char *col_b = reinterpret_cast<const char *>(run_starts + (size_t)b * ntiles);
+        auto bnd = [&](int tt) -> uint32_t {
+            return tt < ntiles ? *reinterpret_cast<const uint32_t *>(col_b + ((uint32_t)rt(tt) << 2)) : 0u;
+        };
+        auto vec = [&](uint32_t tv, uint32_t vi) -> uint4 {
+            return *reinterpret_cast<const uint4 *>(pos_b + ((tv + min(vi, kLastVec)) << 4));
+        };
+        auto tvec = [&](int t) -> uint32_t { return (uint32_t)rt(min(t, ntiles - 1)) << kVecShift; };
+        auto ceil6 = [](uint32_t x) { return (x + 5u) / 6u; };
+        struct St {
+            int t;        // walk step: tile rt(t)
+            uint32_t r;   // its run, start | end << 16 (0: none)
+            uint32_t rn;  // the run of tile t + Q
+            uint32_t vb;  // the group's first vector of this step
+            uint32_t ev;  // the run's end in vectors, ceil(end / 6)
+            uint32_t tv;  // the tile's first vector
+            uint4 v[NV];  // this lane's vectors of the step: vb + sub + G k
+        };
+        auto loads = [&](St &s) {
+#pragma unroll
+            for (int k = 0; k < NV; k++) {
+                const uint32_t vi = s.vb + sub + G * k;
+                s.v[k] = vec(s.tv, REDIR && vi >= s.ev ? s.vb : vi);
+            }
+        };
+        St A, B;
+        A.t = wave * kGroupsPerWave + tl;
+        A.r = bnd(A.t);
+        A.rn = bnd(A.t + Q);
+        A.vb = (A.r & 0xFFFFu) / 6u;
+        A.ev = ceil6(A.r >> 16);
+        A.tv = tvec(A.t);
+        loads(A);
+        // the step after c into n (its loads issued first), then c applied
+        auto step = [&](const St &c, St &n) {
+            const uint32_t vb2 = c.vb + NV * G;
+            const bool adv = vb2 >= c.ev;
+            n.t = adv ? c.t + Q : c.t;
+            n.r = adv ? c.rn : c.r;
+            n.vb = adv ? (c.rn & 0xFFFFu) / 6u : vb2;
+            n.ev = adv ? ceil6(c.rn >> 16) : c.ev;
+            n.tv = adv ? tvec(c.t + Q) : c.tv;
+            n.rn = c.rn;
+            if (adv) n.rn = bnd(c.t + 2 * Q);
+            loads(n);
+            if (c.vb < c.ev) {
+#pragma unroll
+                for (int k = 0; k < NV; k++) apply6(c.v[k], c.t, c.vb + sub + G * k, dec(c.r));
+            }
+        };
+        while (true) {
+            if (__ballot(A.t < ntiles) == 0) break;
+            step(A, B);
+            if (__ballot(B.t < ntiles) == 0) break;
+            step(B, A);
+        }
+    } else if constexpr (WALK == 1 || WALK == 2) {
         // Independent lane groups: group q (G lanes) walks tiles q, q + Q,
         // q + 2Q, ... one step (G vectors) per iteration, moving to its next
         // tile as soon as its run ends, so no group waits for the longest run
@@ -2182,6 +2260,11 @@ hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *w
                 if constexpr (MODE == kApplyBuild || MODE == kApplyBuildL) {
                     if (3 * TK / ws.nbins < 24)
                         return launch_apply_g<MODE, 4, TK, 1, 2>(ws, m, words, nw32, merge, res, st, stream);
+                    // the round-6 walk (WALK 4: C2 pass 2 33.15 -> 32.77 us, C5
+                    // 193.1 -> 192.2, tools/ubench.py p2ab) addresses the sorted
+                    // tiles by 32-bit byte offsets: below 4 GiB of them
+                    if (ws.ntiles * (uint64_t)TK * 8 < (1ull << 32))
+                        return launch_apply_g<MODE, 4, TK, 1, 4>(ws, m, words, nw32, merge, res, st, stream);
                     return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
                 } else
                     return launch_apply_g<MODE, 4, TK>(ws, m, words, nw32, merge, res, st, stream);

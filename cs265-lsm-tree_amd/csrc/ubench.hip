@@ -289,6 +289,40 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
     }
         UB_P2(5001, 512, 511, 4, 2) UB_P2(5003, 512, 511, 6, 3)
 #undef UB_P2
+        // 2500 / 2503: pass 2 of a super-tile build (C4) on the round-6
+        // walk with two vectors per lane (WALK 5) / the product's WALK 3
+        case 2500: case 2503: {
+            if (ws.lad_u || tile_keys_of(ws) != kSuperTileKeys) return -22;
+            const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
+            constexpr int TK = (int)kSuperTileKeys;
+            e = variant == 2500
+                    ? launch_apply_g<kApplyBuild, 4, TK, 1, 5>(ws, mp.m, words, nw32, 0, nullptr, StackTable{}, s)
+                    : launch_apply_g<kApplyBuild, 4, TK, 1, 3>(ws, mp.m, words, nw32, 0, nullptr, StackTable{}, s);
+            break;
+        }
+        // 2400 / 2401: pass 2 of plan_build's one-member ladder (C2, C5) on
+        // the round-6 build walk (WALK 4) / the product's WALK 1, over
+        // variant 0's output
+        case 2400: case 2401: {
+            if (!ws.lad_u || ws.lad_hb != 0 || !mp.p2) return -22;
+            StackTable st{};
+            st.lad.s = ws.lad_s;
+            st.lad.u = ws.lad_u;
+            st.lad.d = mp.p2d;
+            st.lad.t[0] = mp.p2t;
+            st.lad.rinv = ladder0_relabel(mp, ws) ? ladder0_inv(mp) : 0u;
+            const uint64_t nw32 = ((mp.m + 63) / 64) * 2;
+            const size_t tk = tile_keys_of(ws);
+            if (tk == 4096)
+                e = variant == 2400 ? launch_apply_g<kApplyBuildL, 4, 4096, 1, 4>(ws, mp.m, words, nw32, 0, nullptr, st, s)
+                                    : launch_apply_g<kApplyBuildL, 4, 4096, 1, 1>(ws, mp.m, words, nw32, 0, nullptr, st, s);
+            else if (tk == 8192)
+                e = variant == 2400 ? launch_apply_g<kApplyBuildL, 4, 8192, 1, 4>(ws, mp.m, words, nw32, 0, nullptr, st, s)
+                                    : launch_apply_g<kApplyBuildL, 4, 8192, 1, 1>(ws, mp.m, words, nw32, 0, nullptr, st, s);
+            else
+                return -22;
+            break;
+        }
         // 5100 + ABL: the product's C2 pass 1 (plan_build's one-member
         // ladder, 4096-key tiles, three workgroups per CU) cut after a
         // stage (k_part_bin's ABL): the ablation ladder of tools/ubench.py p1abl
