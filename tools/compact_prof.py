@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The bench's fan-in-4 compaction (4 runs x 4.2M entries, filter fused)
 repeated for rocprofv3 --kernel-trace --stats: `python tools/compact_prof.py
-[reps] [alt]` (alt: the lib_alt build of tools/build_alt.sh)."""
+[reps] [alt]` (alt: the lib_alt build of tools/build_alt.sh).  A marker
+kernel separates the setup from the timed calls (tools/trace_stats.py)."""
 import os
 import sys
 import time
@@ -23,6 +24,9 @@ def main():
     total = sum(r.shape[0] for r in runs)
     dout = torch.empty((total, 2), dtype=torch.int32, device="cuda")
     f = bh.BloomFilter(m)
+    bh.compact(druns, drop_tombstones=True, filter=f, out=dout)  # untimed, then the trace marker
+    torch.cuda.synchronize()
+    torch.cuda._sleep(1)
     ts = []
     for _ in range(reps):
         f.clear()

@@ -58,7 +58,7 @@ for s in ${STEPS//,/ }; do
     sq_c3) run sq_c3_a 150 timeout -s KILL 140 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d "$OUT/sq_c3_a" -o pmc --output-format csv -- python tools/probe_prof.py auto 10 || exit 1
            run sq_c3_b 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace -d "$OUT/sq_c3_b" -o pmc --output-format csv -- python tools/probe_prof.py auto 10 || exit 1 ;;
     bench_c5) run bench_c5 400 python bench.py --workload c5 --steps 20 --warmup 3 --no-extras --no-cpu-baseline || exit 1 ;;
-    stats_c2) run stats_c2 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c2" -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline --prewarm-s 0 || exit 1 ;;
+    stats_c2) run stats_c2 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c2" -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
     stats_c4) run stats_c4 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c4" -o run --output-format csv -- python bench.py --workload c4 --steps 5 --warmup 1 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
     stats_c5) run stats_c5 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c5" -o run --output-format csv -- python bench.py --workload c5 --steps 20 --warmup 3 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
     probe_sweep) run probe_sweep 300 python tools/probe_sweep.py || exit 1 ;;

@@ -2,8 +2,9 @@
 """C3 probe (16.8M GETs x 5 level filters) repeated under one strategy, for
 rocprofv3 --kernel-trace --stats: `python tools/probe_prof.py [auto|stacked|
 partition|gather|route] [reps] [alt|-] [c3|f10]` (route: the GET routing,
-bloomhip_route_gets, over runs built with their fences; f10: the f = 10
-tree's three levels instead of C3's five)."""
+bloomhip_route_gets_packed, over runs built with their fences; f10: the f = 10
+tree's three levels instead of C3's five).  A marker kernel separates the
+setup from the timed calls (tools/trace_stats.py)."""
 import os
 import sys
 
@@ -39,13 +40,16 @@ def main():
         filters.append(f)
     out = torch.empty((len(filters), (gets.size + 63) // 64), dtype=torch.int64, device="cuda")
     s = torch.cuda.current_stream()
-    fr = torch.empty(gets.size, dtype=torch.int32, device="cuda")
-    pg = torch.empty(gets.size, dtype=torch.int32, device="cuda")
+    rt = torch.empty(gets.size, dtype=torch.int32, device="cuda")
+    # one untimed call, then the marker kernel tools/trace_stats.py cuts the
+    # trace at (the builds above and this call stay out of the stats)
+    call = (lambda: bh.route_gets_packed(filters, dgets, cand=out, route=rt, stream=s)) if route else \
+        (lambda: bh.test_batch(filters, dgets, out=out, stream=s))
+    call()
+    torch.cuda.synchronize()
+    torch.cuda._sleep(1)
     for _ in range(reps):
-        if route:
-            bh.route_gets(filters, dgets, cand=out, first=fr, page=pg, stream=s)
-        else:
-            bh.test_batch(filters, dgets, out=out, stream=s)
+        call()
     torch.cuda.synchronize()
     print("done", kind, reps)
 
