@@ -1285,8 +1285,10 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         // per lane and step (WALK 5: two, for super-tiles' ~20-entry runs);
         // REDIR (WALK 5, 6: short runs): a lane whose vector lies past the
         // run's end loads the group's first vector instead (WALK 2's note).
-        // Launched: WALK 4 (C2, C5).  WALK 5 against WALK 3 on C4's
-        // super-tiles: 806 against 796 us (profiles/r06/rejected/walk5_c4/).
+        // Not launched: WALK 4 against WALK 1 was 1 % faster in the pass-2
+        // micro-benchmark but 4 % slower in the bench (C2 35.2 -> 36.7 us,
+        // profiles/r06/rejected/walk4_bench/), WALK 5 against WALK 3 on C4's
+        // super-tiles 806 against 796 us (profiles/r06/rejected/walk5_c4/).
         static_assert(!PROBE, "builds");
         constexpr int NV = WALK == 5 ? 2 : 1;
         constexpr bool REDIR = WALK >= 5;
@@ -2260,11 +2262,10 @@ hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *w
                 if constexpr (MODE == kApplyBuild || MODE == kApplyBuildL) {
                     if (3 * TK / ws.nbins < 24)
                         return launch_apply_g<MODE, 4, TK, 1, 2>(ws, m, words, nw32, merge, res, st, stream);
-                    // the round-6 walk (WALK 4: C2 pass 2 33.15 -> 32.77 us, C5
-                    // 193.1 -> 192.2, tools/ubench.py p2ab) addresses the sorted
-                    // tiles by 32-bit byte offsets: below 4 GiB of them
-                    if (ws.ntiles * (uint64_t)TK * 8 < (1ull << 32))
-                        return launch_apply_g<MODE, 4, TK, 1, 4>(ws, m, words, nw32, merge, res, st, stream);
+                    // (round 6's restated walk, WALK 4, was 1 % faster in
+                    // tools/ubench.py p2ab but slower in the bench, where pass 2
+                    // follows pass 1: C2 pass 2 35.2 -> 36.7 us, value 187.6 ->
+                    // 184.6, profiles/r06/rejected/walk4_bench/; not launched)
                     return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
                 } else
                     return launch_apply_g<MODE, 4, TK>(ws, m, words, nw32, merge, res, st, stream);
