@@ -57,6 +57,37 @@ __global__ void ub_lds_or(int iters, uint32_t *sink) {
     if (seg[threadIdx.x] == 0x12345678u) sink[0] = 1;
 }
 
+// Random ds_or with half the lanes idle in five ways (round 6: what pass 2's
+// out-of-run entries cost the LDS): 0 every lane a random word; 1 odd lanes
+// OR 0 into one word shared by the group; 2 odd lanes masked off; 3 odd lanes
+// OR 0 into a private word each; 4 odd lanes OR 0 into a random word (pass
+// 2's branch-free masking).
+template <int MODE>
+__global__ void __launch_bounds__(1024) ub_lds_or_idle(int iters, uint32_t *sink) {
+    extern __shared__ uint32_t seg[];
+    for (int i = threadIdx.x; i < 16384 + 64; i += blockDim.x) seg[i] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const bool idle = MODE != 0 && (lane & 1);
+    uint32_t s = 0x9E3779B9u ^ (blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u;
+    for (int i = 0; i < iters; i++) {
+        const uint32_t r = xorshift(s);
+        uint32_t w = r >> 18, v = 1u << (r & 31);
+        if (idle) {
+            v = 0;
+            if constexpr (MODE == 1) w = 16384;
+            if constexpr (MODE == 3) w = 16384 + lane;
+        }
+        if constexpr (MODE == 2) {
+            if (!idle) atomicOr(&seg[w], v);
+        } else {
+            atomicOr(&seg[w], v);
+        }
+    }
+    __syncthreads();
+    if (seg[threadIdx.x] == 0x12345678u) sink[0] = 1;
+}
+
 __global__ void ub_hash(ModParams mp, int iters, uint32_t *sink) {
     uint32_t acc = 0;
     int32_t k = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u);
@@ -174,6 +205,11 @@ extern "C" int ubench_run(int which, void *dbuf, size_t bytes, uint64_t m, int g
             break;
         }
         case 6: ub_stream<<<grid, block, 0, s>>>(reinterpret_cast<const uint4 *>(dbuf), bytes / 16 - 1, sink); break;
+        case 40: ub_lds_or_idle<0><<<grid, 1024, 66 * 1024, s>>>(iters, sink); break;
+        case 41: ub_lds_or_idle<1><<<grid, 1024, 66 * 1024, s>>>(iters, sink); break;
+        case 42: ub_lds_or_idle<2><<<grid, 1024, 66 * 1024, s>>>(iters, sink); break;
+        case 43: ub_lds_or_idle<3><<<grid, 1024, 66 * 1024, s>>>(iters, sink); break;
+        case 44: ub_lds_or_idle<4><<<grid, 1024, 66 * 1024, s>>>(iters, sink); break;
         case 10: case 11: case 12:  // block = waves doing VALU (of 16), iters = hash iters
             ub_mixed<0><<<grid, 1024, 65536, s>>>(make_mod_params(167772160), block, which - 10,
                                                   iters, iters * 6, sink);

@@ -547,6 +547,17 @@ def main():
         size = {"p2ab": (16_777_216, 10.0, 50), "p2ab_c5": (67_108_864, 10.0, 20),
                 "p2ab_c4": (268_435_456, 12.0, 5)}[sys.argv[1]]
         return p2_ab(vs, *size)
+    if len(sys.argv) > 1 and sys.argv[1] == "ldsidle":
+        buf = torch.zeros(1 << 20, dtype=torch.int32, device="cuda")
+        names = {40: "all lanes random", 41: "odd lanes OR 0 into one shared word",
+                 42: "odd lanes masked off", 43: "odd lanes OR 0 into private words",
+                 44: "odd lanes OR 0 into random words"}
+        for rnd in range(3):
+            for v, nm in names.items():
+                ms = timeit(v, buf, buf.numel() * 4, 0, 512, 1024, 256)
+                print(json.dumps({"op": "lds_or idle lanes", "variant": v, "mode": nm, "round": rnd,
+                                  "ms": round(ms, 4)}), flush=True)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "p1abl":
         return p1_ablation()
     if len(sys.argv) > 1 and sys.argv[1] == "p1tail":
