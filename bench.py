@@ -253,13 +253,13 @@ def time_leg(call, torch, prewarm_s=LEG_PREWARM_S, calls=LEG_MIN_CALLS, sync=Non
     return (time.perf_counter() - t0) / max(calls, 1), n
 
 
-COMPUTE_CEILING = os.path.join("profiles", "r05", "compute_ceiling.json")
+COMPUTE_CEILING = os.path.join("profiles", "r06", "compute_ceiling.json")
 
 
 def compute_ceiling(case, achieved):
     """The VALU ceiling of a workload's pass 1 (tools/ubench.py prim: the three
     hashes plus each position's bin and entry exactly as k_part_bin forms
-    them for this geometry, compute only; profiles/r05/compute_ceiling.json)
+    them for this geometry, compute only; profiles/r06/compute_ceiling.json)
     beside the achieved rate: the build cannot beat its own arithmetic."""
     path = os.path.join(ROOT, COMPUTE_CEILING)
     if not os.path.exists(path):

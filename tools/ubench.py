@@ -437,7 +437,7 @@ LIB.ubench_pass1_arith.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, 
                                    ctypes.POINTER(ctypes.c_int)]
 LIB.ubench_pass1_arith.restype = ctypes.c_int
 MK_NAMES = {0: "mod_fast (segments)", 1: "mod_wide (segments)", 2: "p2 (segments)",
-            3: "ladder stack", 4: "ladder build"}
+            3: "ladder stack", 4: "ladder build", 5: "ladder build, block (x >> 24) % d"}
 # the product's geometries: (name, filter sizes); one size = a build, several = a stacked probe
 PASS1_CASES = [("C2 build", [167_772_160]), ("C5 build", [671_088_640]),
                ("C4 build", [3_221_225_472]), ("C3 probe (5-level ladder)",
