@@ -446,8 +446,10 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
             const uint2 a = src[0], b = src[1], c = src[2];
             uint32_t e[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
             if constexpr (!FULL) {
+                // past the tile's positions: 0, not stale (the ladder probe's
+                // pass 2 reads with every entry of a vector, its run's or not)
 #pragma unroll
-                for (int q = 0; q < 6; q++) e[q] &= kEntryMask;
+                for (int q = 0; q < 6; q++) e[q] = 6 * (r * TB + tid) + q < 3 * tile_keys ? e[q] & kEntryMask : 0u;
             }
             // (a << s) | b is one v_lshl_or_b32; the compiler emitted a shift
             // and an or for each (5 instead of 3 per u64)
@@ -1159,11 +1161,17 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                 }
             }
         } else {
-            uint32_t bits[6], mask = 0;
+            // the run's entries among the six, as the build's 6-bit mask
+            // (round 6: once per vector instead of a compare and an OR per entry)
+            const int s0 = (int)(6 * vi) - (int)r.x;
+            const int lo = max(-s0, 0), hi = min(max((int)r.y - (int)(6 * vi), 0), 6);
+            const uint32_t mask = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+            (void)i0;
+            (void)len;
+            uint32_t bits[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) {
-                const uint32_t ok = i0 + k < len ? 1u : 0u;
-                mask |= ok << k;
+                const uint32_t ok = __builtin_amdgcn_ubfe(mask, k, 1);
                 if constexpr (MODE == kApplyLadder) {
                     // member 0's block is the entry's high part (its blocks
                     // come first at LDS 0, 2^(s-3) bytes each), so its word's
@@ -1175,7 +1183,13 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                     const LadderTable &L = st.lad;
                     constexpr int K = LK == 0 ? 1 : LK;  // direct members, compiled in
                     constexpr bool CT = LK == 0;          // packed tuple computed, no table
-                    const uint32_t ee = ok ? e[k] : 0u;  // reads stay in the image
+                    // An entry outside the run is another run's (or 0 past a
+                    // short tile's end: k_part_bin writes zeros there), so
+                    // its high part is a block this bin stages and its reads
+                    // stay in the image; its result bits are not stored
+                    // (round 6: the select cost a VALU per entry)
+                    const uint32_t ee = e[k];
+                    (void)ok;
                     const uint32_t a0 = (ee >> 3) & ~3u;
                     uint32_t acc = __builtin_amdgcn_ubfe(lds_word(a0), ee, 1u);
                     if constexpr (CT) {
@@ -1272,7 +1286,7 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         }
     };
 
-    if constexpr (WALK >= 4) {
+    if constexpr (WALK >= 4 && WALK <= 6) {
         // WALK 1 / 3 / 2's walks for builds (round 6: WALK 4 / 5 / 6),
         // restated for fewer instructions per step: unrolled over two
         // register sets (the old loops copy their carried state at the
@@ -1389,6 +1403,72 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
             const uint4 v2 = load(min(t2, ntiles - 1), vload(vb2 + sub, vb2, r2 >> 16));
             if (t < ntiles && 6 * vb < (r >> 16)) apply6(v, t, vb + sub, dec(r));
             t = t2; r = r2; rn = rn2; vb = vb2; v = v2;
+        }
+    } else if constexpr (WALK >= 7) {
+        // WALK 3 on two interleaved chains per lane group (round 6): chain c
+        // walks the group's tiles q + c Q, q + (2 + c) Q, ..., both chains'
+        // next vectors in flight together, so a lane holds four 16-B loads
+        // and two run-bound loads in flight instead of two and one (C4's
+        // entries come from HBM, not the Infinity Cache: its pass 2 waits on
+        // load latency, one (tile, segment) pair per group step).
+        constexpr int kGroupsPerWave = 64 / G;
+        const int Q = kGroupsPerWave * (BLOCK / 64);
+        constexpr int NC = WALK - 5;  // WALK 7: 2 chains (launched), 8: 3, 9: 4 (slower)
+        auto bnd = [&](int tt) -> uint32_t {
+            return tt < ntiles ? run_starts[(size_t)b * ntiles + rt(tt)] : 0u;
+        };
+        int t[NC];
+        uint32_t r[NC], rn[NC], vb[NC];
+        uint4 v[NC], w[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            t[c] = wave * kGroupsPerWave + tl + c * Q;
+            r[c] = bnd(t[c]);
+            rn[c] = bnd(t[c] + NC * Q);
+            vb[c] = (r[c] & 0xFFFFu) / 6u;
+            v[c] = load(min(t[c], ntiles - 1), vload(vb[c] + sub, vb[c], r[c] >> 16));
+            w[c] = load(min(t[c], ntiles - 1), vload(vb[c] + G + sub, vb[c], r[c] >> 16));
+        }
+        auto live = [&]() {
+            bool any = false;
+#pragma unroll
+            for (int c = 0; c < NC; c++) any |= t[c] < ntiles;
+            return any;
+        };
+        while (__ballot(live()) != 0) {
+            int t2[NC];
+            uint32_t r2[NC], rn2[NC], vb2[NC];
+            uint4 v2[NC], w2[NC];
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                t2[c] = t[c];
+                r2[c] = r[c];
+                vb2[c] = vb[c] + 2 * G;
+                const bool adv = 6 * vb2[c] >= (r[c] >> 16);
+                if (adv) {
+                    t2[c] += NC * Q;
+                    r2[c] = rn[c];
+                    vb2[c] = (r2[c] & 0xFFFFu) / 6u;
+                }
+                rn2[c] = rn[c];
+                if (adv) rn2[c] = bnd(t2[c] + NC * Q);
+            }
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                v2[c] = load(min(t2[c], ntiles - 1), vload(vb2[c] + sub, vb2[c], r2[c] >> 16));
+                w2[c] = load(min(t2[c], ntiles - 1), vload(vb2[c] + G + sub, vb2[c], r2[c] >> 16));
+            }
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                if (t[c] < ntiles && 6 * vb[c] < (r[c] >> 16)) {
+                    apply6(v[c], t[c], vb[c] + sub, dec(r[c]));
+                    apply6(w[c], t[c], vb[c] + G + sub, dec(r[c]));
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                t[c] = t2[c]; r[c] = r2[c]; rn[c] = rn2[c]; vb[c] = vb2[c]; v[c] = v2[c]; w[c] = w2[c];
+            }
         }
     } else if constexpr (WALK == 3) {
         // The same walk with two vectors per lane per step (vectors vb + sub
@@ -2284,8 +2364,11 @@ hipError_t launch_apply(const PartitionWorkspace &ws, uint64_t m, uint32_t *word
             // super-tiles: >= kSuperMinBins segments, runs of at most 48
             // entries on average: independent groups of 4 lanes
             constexpr int TK = (int)kSuperTileKeys;
+            // short runs: two vectors per lane, on two interleaved chains per
+            // lane group (WALK 7: C4 pass 2 795 -> 764 us; three chains 875,
+            // four 916, profiles/r06/c4_two_chains/)
             if (3 * TK / ws.nbins < 24)
-                return launch_apply_g<MODE, 4, TK, 1, 3>(ws, m, words, nw32, merge, res, st, stream);
+                return launch_apply_g<MODE, 4, TK, 1, 7>(ws, m, words, nw32, merge, res, st, stream);
             return launch_apply_g<MODE, 4, TK, 1, 1>(ws, m, words, nw32, merge, res, st, stream);
         }
     } else if constexpr (MODE == kApplyStack) {
