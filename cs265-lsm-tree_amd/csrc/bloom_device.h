@@ -1410,24 +1410,31 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         // next vectors in flight together, so a lane holds four 16-B loads
         // and two run-bound loads in flight instead of two and one (C4's
         // entries come from HBM, not the Infinity Cache: its pass 2 waits on
-        // load latency, one (tile, segment) pair per group step).
+        // load latency, one (tile, segment) pair per group step).  WALK 10:
+        // WALK 1 (one vector per lane, no redirect) on two chains.
         constexpr int kGroupsPerWave = 64 / G;
         const int Q = kGroupsPerWave * (BLOCK / 64);
-        constexpr int NC = WALK - 5;  // WALK 7: 2 chains (launched), 8: 3, 9: 4 (slower)
+        constexpr int NC = WALK == 10 ? 2 : WALK - 5;  // WALK 7: 2 chains (launched), 8: 3, 9: 4 (slower)
+        constexpr int NV = WALK == 10 ? 1 : 2;          // vectors per lane and step
+        auto vl = [&](uint32_t vi, uint32_t vb, uint32_t end) -> uint32_t {
+            if constexpr (WALK == 10) return vi;
+            return vload(vi, vb, end);
+        };
         auto bnd = [&](int tt) -> uint32_t {
             return tt < ntiles ? run_starts[(size_t)b * ntiles + rt(tt)] : 0u;
         };
         int t[NC];
         uint32_t r[NC], rn[NC], vb[NC];
-        uint4 v[NC], w[NC];
+        uint4 v[NC][NV];
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             t[c] = wave * kGroupsPerWave + tl + c * Q;
             r[c] = bnd(t[c]);
             rn[c] = bnd(t[c] + NC * Q);
             vb[c] = (r[c] & 0xFFFFu) / 6u;
-            v[c] = load(min(t[c], ntiles - 1), vload(vb[c] + sub, vb[c], r[c] >> 16));
-            w[c] = load(min(t[c], ntiles - 1), vload(vb[c] + G + sub, vb[c], r[c] >> 16));
+#pragma unroll
+            for (int k = 0; k < NV; k++)
+                v[c][k] = load(min(t[c], ntiles - 1), vl(vb[c] + k * G + sub, vb[c], r[c] >> 16));
         }
         auto live = [&]() {
             bool any = false;
@@ -1438,12 +1445,12 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         while (__ballot(live()) != 0) {
             int t2[NC];
             uint32_t r2[NC], rn2[NC], vb2[NC];
-            uint4 v2[NC], w2[NC];
+            uint4 v2[NC][NV];
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 t2[c] = t[c];
                 r2[c] = r[c];
-                vb2[c] = vb[c] + 2 * G;
+                vb2[c] = vb[c] + NV * G;
                 const bool adv = 6 * vb2[c] >= (r[c] >> 16);
                 if (adv) {
                     t2[c] += NC * Q;
@@ -1454,20 +1461,22 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
                 if (adv) rn2[c] = bnd(t2[c] + NC * Q);
             }
 #pragma unroll
-            for (int c = 0; c < NC; c++) {
-                v2[c] = load(min(t2[c], ntiles - 1), vload(vb2[c] + sub, vb2[c], r2[c] >> 16));
-                w2[c] = load(min(t2[c], ntiles - 1), vload(vb2[c] + G + sub, vb2[c], r2[c] >> 16));
-            }
+            for (int c = 0; c < NC; c++)
+#pragma unroll
+                for (int k = 0; k < NV; k++)
+                    v2[c][k] = load(min(t2[c], ntiles - 1), vl(vb2[c] + k * G + sub, vb2[c], r2[c] >> 16));
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 if (t[c] < ntiles && 6 * vb[c] < (r[c] >> 16)) {
-                    apply6(v[c], t[c], vb[c] + sub, dec(r[c]));
-                    apply6(w[c], t[c], vb[c] + G + sub, dec(r[c]));
+#pragma unroll
+                    for (int k = 0; k < NV; k++) apply6(v[c][k], t[c], vb[c] + k * G + sub, dec(r[c]));
                 }
             }
 #pragma unroll
             for (int c = 0; c < NC; c++) {
-                t[c] = t2[c]; r[c] = r2[c]; rn[c] = rn2[c]; vb[c] = vb2[c]; v[c] = v2[c]; w[c] = w2[c];
+                t[c] = t2[c]; r[c] = r2[c]; rn[c] = rn2[c]; vb[c] = vb2[c];
+#pragma unroll
+                for (int k = 0; k < NV; k++) v[c][k] = v2[c][k];
             }
         }
     } else if constexpr (WALK == 3) {
