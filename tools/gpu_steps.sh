@@ -71,6 +71,9 @@ for s in ${STEPS//,/ }; do
     stats_c3_alt) run stats_c3_alt 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3_alt" -o run --output-format csv -- python tools/probe_prof.py auto 30 alt || exit 1 ;;
     stats_route) run stats_route 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_route" -o run --output-format csv -- python tools/probe_prof.py route 30 || exit 1 ;;
     stats_f10) run stats_f10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_f10" -o run --output-format csv -- python tools/probe_prof.py auto 30 - f10 || exit 1 ;;
+    stats_route_f10) run stats_route_f10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_route_f10" -o run --output-format csv -- python tools/probe_prof.py route 30 - f10 || exit 1 ;;
+    bench_rep) run bench_rep1 600 python bench.py || exit 1
+               run bench_rep2 600 python bench.py || exit 1 ;;
     stats_c3) run stats_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3" -o run --output-format csv -- python tools/probe_prof.py auto 30 || exit 1 ;;
     pmc_c2) pmc c2 FETCH_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
             pmc c2 WRITE_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;
