@@ -74,6 +74,10 @@ for s in ${STEPS//,/ }; do
     stats_route_f10) run stats_route_f10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_route_f10" -o run --output-format csv -- python tools/probe_prof.py route 30 - f10 || exit 1 ;;
     bench_rep) run bench_rep1 600 python bench.py || exit 1
                run bench_rep2 600 python bench.py || exit 1 ;;
+    sq_route) for w in c3 f10; do
+                run sq_route_${w}_a 150 timeout -s KILL 140 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d "$OUT/sq_route_${w}_a" -o pmc --output-format csv -- python tools/probe_prof.py route 10 - $w || exit 1
+                run sq_route_${w}_b 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace -d "$OUT/sq_route_${w}_b" -o pmc --output-format csv -- python tools/probe_prof.py route 10 - $w || exit 1
+              done ;;
     stats_c3) run stats_c3 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_c3" -o run --output-format csv -- python tools/probe_prof.py auto 30 || exit 1 ;;
     pmc_c2) pmc c2 FETCH_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1
             pmc c2 WRITE_SIZE --steps 10 --warmup 2 --no-cpu-baseline --no-extras --prewarm-s 0 || exit 1 ;;

@@ -8,7 +8,7 @@ import re
 import subprocess
 import sys
 
-S = "cs265-lsm-tree_amd/lib/obj/bloom_kernels-hip-amdgcn-amd-amdhsa-gfx950.s"
+S = sys.argv[3] if len(sys.argv) > 3 else "cs265-lsm-tree_amd/lib/obj/bloom_kernels-hip-amdgcn-amd-amdhsa-gfx950.s"
 want = sys.argv[1]
 lines = open(S).read().splitlines()
 # kernel bodies start at "<mangled>:" labels of functions marked @function

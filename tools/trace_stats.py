@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-kernel stats of ONE workload's timed calls from a rocprofv3
 --kernel-trace CSV: the dispatches after the last marker kernel (the
-profiling scripts launch torch.cuda._sleep(1) between their setup -- filter
+profiling scripts launch torch.cuda._sleep(1), whose kernel is torch's
+spin_kernel, between their setup -- filter
 builds, key uploads -- and the timed calls), grouped by kernel name, written
 in the layout of rocprofv3's --stats kernel CSV (Name, Calls, TotalDurationNs,
 AverageNs, Percentage, MinNs, MaxNs).  Without a marker every dispatch counts.
@@ -15,7 +16,7 @@ def main(src, dst):
     rows = sorted(csv.DictReader(open(src)), key=lambda r: int(r["Start_Timestamp"]))
     last = -1
     for i, r in enumerate(rows):
-        if "sleep" in r["Kernel_Name"].lower():
+        if "spin_kernel" in r["Kernel_Name"] or "sleep" in r["Kernel_Name"].lower():
             last = i
     durs = collections.defaultdict(list)
     for r in rows[last + 1:]:
