@@ -1752,22 +1752,39 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
     static_assert(kPasses * BLOCK * kCombineKeys == TILE_KEYS, "8 keys per thread and pass");
     extern __shared__ int32_t s_fences[];
     __shared__ __attribute__((aligned(16))) uint8_t s_r[kTilePos];
-    __shared__ int32_t s_lo[kMaxStack], s_hi[kMaxStack];
-    __shared__ uint32_t s_nf[kMaxStack], s_off[kMaxStack];
-    __shared__ float s_f0[kMaxStack], s_scale[kMaxStack];
+    // per run: its fences' LDS offset and count, first fence and fence
+    // spacing (one 16-B read per routed key); per member: its run's key
+    // range as a window, k - lo <= span in u32 (one broadcast read per member
+    // and pass of 8 keys)
+    __shared__ __attribute__((aligned(16))) uint4 s_rec[kMaxStack];
+    __shared__ __attribute__((aligned(8))) uint2 s_win[kMaxStack];
     __shared__ int s_run_of[kMaxStack];
     const int nf = rows.nf;
     for (int r = threadIdx.x; r < nf; r += BLOCK) {
         const uint32_t n = rt.nfences[r];
         const int32_t f0 = n ? rt.meta[r][1] : 0, fl = n ? rt.meta[r][n] : 0;
-        s_hi[r] = n ? rt.meta[r][0] : INT32_MIN;  // no fences: never in range
-        s_lo[r] = n ? f0 : INT32_MAX;
-        s_nf[r] = n;
-        s_off[r] = rt.fence_off[r];
-        s_f0[r] = (float)f0;
-        s_scale[r] = (n > 1 && fl > f0) ? (float)(n - 1) / ((float)fl - (float)f0) : 0.0f;
+        const float scale = (n > 1 && fl > f0) ? (float)(n - 1) / ((float)fl - (float)f0) : 0.0f;
+        s_rec[r] = make_uint4(rt.fence_off[r], n, __float_as_uint((float)f0), __float_as_uint(scale));
         s_run_of[r] = rows.row[r];
+        const int rr = rows.row[r];  // member r's run: [first fence, max key]
+        const uint32_t nr = rt.nfences[rr];
+        const int32_t lo = nr ? rt.meta[rr][1] : 0, hi = nr ? rt.meta[rr][0] : 0;
+        s_win[r] = make_uint2((uint32_t)lo, (uint32_t)hi - (uint32_t)lo);  // (a dead window: live below)
     }
+    // members whose run has keys in range at all (no fences, or max key
+    // below the first fence: never in range), and whether member j is run j
+    uint32_t live = 0;
+    bool ident = true;
+#pragma unroll
+    for (int j = 0; j < kMaxStack; j++) {
+        if (j < nf) {
+            const int r = rows.row[j];
+            const uint32_t n = rt.nfences[r];
+            if (n && rt.meta[r][0] >= rt.meta[r][1]) live |= 1u << j;
+            ident &= r == j;
+        }
+    }
+    const uint32_t live4 = live * 0x01010101u;
     {
         // every run's fences, contiguous in LDS (fence_off is the prefix of
         // the counts), 8 loads in flight per thread (a load-then-store loop
@@ -1850,7 +1867,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
         }
         const uint32_t a[4] = {va.x, va.y, va.z, va.w}, b[4] = {vb.x, vb.y, vb.z, vb.w},
                        c[4] = {vc.x, vc.y, vc.z, vc.w};
-        uint32_t cand_lo = 0, cand_hi = 0;  // byte i: key i's candidate runs (bit r: filter and range)
+        // byte i: key i's member bits, then its candidate runs (bit r: filter and range)
+        uint32_t cand_lo = 0, cand_hi = 0, in_lo = 0, in_hi = 0;
         int32_t fr[kCombineKeys], pg[kCombineKeys];
 #pragma unroll
         for (int i = 0; i < kCombineKeys; i++) {
@@ -1861,17 +1879,40 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
                                                                  s_r[min(sb, (uint32_t)kTilePos - 1)] &
                                                                  s_r[min(sc, (uint32_t)kTilePos - 1)])
                                                     : 0u;
-            uint32_t m = 0;
+            if (i < 4) cand_lo |= hit << (8 * i);
+            else cand_hi |= hit << (8 * (i - 4));
+        }
+        // the range checks, member by member over the 8 keys (k - lo <= span)
+#pragma unroll
+        for (int j = 0; j < kMaxStack; j++) {
+            if (j < nf) {
+                const uint2 w = s_win[j];
+#pragma unroll
+                for (int i = 0; i < kCombineKeys; i++) {
+                    const uint32_t in = (uint32_t)key[i] - w.x <= w.y ? 1u << (8 * (i & 3) + j) : 0u;
+                    if (i < 4) in_lo |= in;
+                    else in_hi |= in;
+                }
+            }
+        }
+        cand_lo &= in_lo & live4;
+        cand_hi &= in_hi & live4;
+        if (!ident) {  // member j is run rows.row[j]: move its bits
+            const uint32_t ml = cand_lo, mh = cand_hi;
+            cand_lo = cand_hi = 0;
 #pragma unroll
             for (int j = 0; j < kMaxStack; j++) {
                 if (j < nf) {
-                    const int r = s_run_of[j];
-                    const bool in = key[i] >= s_lo[r] && key[i] <= s_hi[r];
-                    m |= (((hit >> j) & 1u) & (uint32_t)in) << r;
+                    const int sh = s_run_of[j] - j;
+                    const uint32_t bl = ml & (0x01010101u << j), bh = mh & (0x01010101u << j);
+                    cand_lo |= sh >= 0 ? bl << sh : bl >> -sh;
+                    cand_hi |= sh >= 0 ? bh << sh : bh >> -sh;
                 }
             }
-            if (i < 4) cand_lo |= m << (8 * i);
-            else cand_hi |= m << (8 * (i - 4));
+        }
+#pragma unroll
+        for (int i = 0; i < kCombineKeys; i++) {
+            const uint32_t m = ((i < 4 ? cand_lo : cand_hi) >> (8 * (i & 3))) & 0xFFu;
             fr[i] = m ? __builtin_ctz(m) : -1;  // runs newest first: the lowest bit
         }
         // The pages of the lane's keys, two searched side by side (their LDS
@@ -1887,13 +1928,14 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
 #pragma unroll
             for (int u = 0; u < kSide; u++) {
                 const int i = h + u;
-                const int r = max(fr[i], 0);
-                base_[u] = (int)s_off[r];
-                n_[u] = fr[i] >= 0 ? (int)s_nf[r] : 0;
+                const uint4 rec = s_rec[max(fr[i], 0)];
+                base_[u] = (int)rec.x;
+                n_[u] = fr[i] >= 0 ? (int)rec.y : 0;
                 int a = 0;
                 ok_[u] = true;
                 if (n_[u] > kFusedWindow) {
-                    const int g = (int)fminf(fmaxf(((float)key[i] - s_f0[r]) * s_scale[r], 0.0f), kGuessMax);
+                    const int g = (int)fminf(fmaxf(((float)key[i] - __uint_as_float(rec.z)) * __uint_as_float(rec.w), 0.0f),
+                                             kGuessMax);
                     a = min(max(g - kFusedWindow / 2, 0), n_[u] - kFusedWindow);
                     const int32_t fl = s_fences[base_[u] + max(a - 1, 0)];
                     const int32_t fh = s_fences[base_[u] + min(a + kFusedWindow, n_[u] - 1)];

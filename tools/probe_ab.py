@@ -21,7 +21,7 @@ sys.path.insert(0, sys.argv[1])
 import torch
 import bloomhip as bh
 from bloomhip import workloads as W
-gets, levels = W.c3() if sys.argv[2] == "c3" else W.f10()
+gets, levels = W.c3_runs() if sys.argv[2] == "c3" else W.f10_runs()  # runs sorted, as written (fences)
 dg = torch.from_numpy(gets).cuda()
 fs = []
 for _, keys, m in levels:

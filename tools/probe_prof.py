@@ -27,7 +27,12 @@ def main():
           "gather": bh.PROBE_GATHER}[kind]
     torch.cuda.set_device(0)
     workload = sys.argv[4] if len(sys.argv) > 4 else "c3"
-    gets, levels = W.c3() if workload == "c3" else W.f10()
+    # routing needs each run as the reference writes it (sorted: its fences
+    # ascend); the filters are the same either way
+    if route:
+        gets, levels = W.c3_runs() if workload == "c3" else W.f10_runs()
+    else:
+        gets, levels = W.c3() if workload == "c3" else W.f10()
     dgets = torch.from_numpy(gets).cuda()
     filters = []
     for lvl, keys, m in levels:
