@@ -2393,6 +2393,13 @@ hipError_t launch_apply_tk(const PartitionWorkspace &ws, uint64_t m, uint32_t *w
                 if constexpr (MODE == kApplyBuild || MODE == kApplyBuildL) {
                     if (3 * TK / ws.nbins < 24)
                         return launch_apply_g<MODE, 4, TK, 1, 2>(ws, m, words, nw32, merge, res, st, stream);
+                    // entries beyond the Infinity Cache (C5: 512 MiB, read
+                    // from HBM): two vectors per lane and step, so a ~48-entry
+                    // run is one step with twice the loads in flight (C5 pass 2
+                    // 192.5 -> 173.6 us, tools/ubench.py p2ab_c5; C2's 128 MiB
+                    // equal either way, so it keeps WALK 1)
+                    if ((uint64_t)ws.ntiles * TK * 8 > kInfinityCacheBytes)
+                        return launch_apply_g<MODE, 4, TK, 1, 3>(ws, m, words, nw32, merge, res, st, stream);
                     // (round 6's restated walk, WALK 4, was 1 % faster in
                     // tools/ubench.py p2ab but slower in the bench, where pass 2
                     // follows pass 1: C2 pass 2 35.2 -> 36.7 us, value 187.6 ->

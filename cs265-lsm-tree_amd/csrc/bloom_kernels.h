@@ -221,6 +221,8 @@ constexpr size_t kProbePartitionMinKeys = 1u << 18;
 // member j's segment b % (m_j / w) at the same offset o.  Pass 2 holds the w-bit
 // segment of every member in LDS and writes one result byte per sorted entry
 // (bit j = member j's bit); the combine ANDs each key's three bytes.
+// MI355X's Infinity Cache (MALL): a pass-2 input larger than this comes from HBM
+constexpr uint64_t kInfinityCacheBytes = 256ull << 20;
 constexpr int kMaxStack = 8;
 
 // Ladder stack: every member is m_j = d << t_j with the same odd d | 255

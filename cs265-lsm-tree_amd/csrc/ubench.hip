@@ -352,7 +352,7 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
         // 2400 / 2401: pass 2 of plan_build's one-member ladder (C2, C5) on
         // the round-6 build walk (WALK 4) / the product's WALK 1, over
         // variant 0's output
-        case 2400: case 2401: case 2410: {
+        case 2400: case 2401: case 2410: case 2413: case 2417: {
             if (!ws.lad_u || ws.lad_hb != 0 || !mp.p2) return -22;
             StackTable st{};
             st.lad.s = ws.lad_s;
@@ -365,10 +365,14 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
             if (tk == 4096)
                 e = variant == 2400 ? launch_apply_g<kApplyBuildL, 4, 4096, 1, 4>(ws, mp.m, words, nw32, 0, nullptr, st, s)
                   : variant == 2410 ? launch_apply_g<kApplyBuildL, 4, 4096, 1, 10>(ws, mp.m, words, nw32, 0, nullptr, st, s)
+                  : variant == 2413 ? launch_apply_g<kApplyBuildL, 4, 4096, 1, 3>(ws, mp.m, words, nw32, 0, nullptr, st, s)
+                  : variant == 2417 ? launch_apply_g<kApplyBuildL, 4, 4096, 1, 7>(ws, mp.m, words, nw32, 0, nullptr, st, s)
                                     : launch_apply_g<kApplyBuildL, 4, 4096, 1, 1>(ws, mp.m, words, nw32, 0, nullptr, st, s);
             else if (tk == 8192)
                 e = variant == 2400 ? launch_apply_g<kApplyBuildL, 4, 8192, 1, 4>(ws, mp.m, words, nw32, 0, nullptr, st, s)
                   : variant == 2410 ? launch_apply_g<kApplyBuildL, 4, 8192, 1, 10>(ws, mp.m, words, nw32, 0, nullptr, st, s)
+                  : variant == 2413 ? launch_apply_g<kApplyBuildL, 4, 8192, 1, 3>(ws, mp.m, words, nw32, 0, nullptr, st, s)
+                  : variant == 2417 ? launch_apply_g<kApplyBuildL, 4, 8192, 1, 7>(ws, mp.m, words, nw32, 0, nullptr, st, s)
                                     : launch_apply_g<kApplyBuildL, 4, 8192, 1, 1>(ws, mp.m, words, nw32, 0, nullptr, st, s);
             else
                 return -22;
