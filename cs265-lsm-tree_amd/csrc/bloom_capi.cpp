@@ -837,13 +837,12 @@ int probe_stacks(bloomhip_filter *f0, const bloomhip_filter *const *filters, int
         // in its combine (k_probe_combine_route), not in k_route afterwards
         const bool fuse = route && (int)mem.size() == nf && route->rt->nruns == nf &&
                           (size_t)route->rt->total_fences * 4 <= kRouteLdsFenceBytesMax;
-        // The fused combine on super-tiles stages 48 KiB of result bytes per
-        // tile: when that and the fences leave one workgroup per CU, 8192-key
-        // tiles (two per CU) route faster (the f = 10 tree: 0.351 against
-        // 0.387 ms, while its plain probe gains from super-tiles)
-        if (fuse && ws.tile_keys == kSuperTileKeys &&
-            2 * combine_route_lds_bytes(route->rt->total_fences, kSuperTileKeys) > kLdsBitmapBytes)
-            ws.tile_keys = 0;
+        // (The fused combine on super-tiles stages 48 KiB of result bytes per
+        // tile, which with the f = 10 tree's fences leaves one workgroup per
+        // CU; round 5 routed such stacks on 8192-key tiles instead, 0.351
+        // against 0.387 ms. Since the combine's range check reads one window
+        // per member (round 6), super-tiles route that tree faster: 0.3126 ->
+        // 0.3093 ms, profiles/r06/route_super_tiles/.)
         const LockedWorkspace w(f0->device, s);
         int rc = partition_buffers(w.get(), n, s, &ws);
         if (rc) return rc;
