@@ -575,6 +575,20 @@ def test_c4_full_bitmap(golden):
     assert unpack_bools(got, keys[::97].size).all()
 
 
+@pytest.mark.parametrize("m", [671_088_640, 360_000_007])
+def test_hbm_resident_pass2_ragged(coracle, m):
+    """Builds whose sorted entries exceed the Infinity Cache (> 256 MiB, more
+    than 33.5M keys) walk pass 2 with two vectors per lane (WALK 3): a ragged
+    batch (a short last tile) on C5's ladder geometry (5 << 27) and on a
+    general m (segments), against the oracle."""
+    n = 33_554_432 + 3 * 8192 + 777
+    keys = rand_keys(n, seed=m % 101)
+    f = bh.BloomFilter(m)
+    f.set_strategy(bh.BUILD_PARTITION)
+    f.set_batch(keys)
+    assert (f.words() == coracle.build(m, keys)).all()
+
+
 def test_c5_run0_full_bitmap(golden):
     from bloomhip import workloads as W
     keys, m = W.c5_run(0)
