@@ -327,7 +327,7 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
 #undef UB_P2
         // 2500 / 2503: pass 2 of a super-tile build (C4) on the round-6
         // walk with two vectors per lane (WALK 5) / the product's WALK 3
-        case 2500: case 2503: case 2523: case 2522: case 2507: case 2508: case 2509: {
+        case 2500: case 2503: case 2523: case 2522: case 2507: case 2508: case 2509: case 2511: {
             // 2523 / 2522: WALK 3 at G = 2 lanes per tile (24 entries a step
             // for C4's ~20-entry runs) / WALK 2 (one vector) at G = 4
             if (ws.lad_u || tile_keys_of(ws) != kSuperTileKeys) return -22;
@@ -345,6 +345,8 @@ extern "C" int ubench_part(int variant, const void *keys, size_t n, uint64_t m, 
                 e = launch_apply_g<kApplyBuild, 4, TK, 1, 9>(ws, mp.m, words, nw32, 0, nullptr, StackTable{}, s);
             else if (variant == 2523)
                 e = launch_apply_g<kApplyBuild, 2, TK, 1, 3>(ws, mp.m, words, nw32, 0, nullptr, StackTable{}, s);
+            else if (variant == 2511)  // two chains of one redirected vector per lane
+                e = launch_apply_g<kApplyBuild, 4, TK, 1, 11>(ws, mp.m, words, nw32, 0, nullptr, StackTable{}, s);
             else
                 e = launch_apply_g<kApplyBuild, 4, TK, 1, 2>(ws, mp.m, words, nw32, 0, nullptr, StackTable{}, s);
             break;
