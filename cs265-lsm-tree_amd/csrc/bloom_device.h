@@ -264,13 +264,20 @@ __device__ __forceinline__ void bin_entry(uint64_t raw, const ModParams &mp, con
     }
 }
 
+// A 16-B non-temporal store (pass 1's sorted tiles beyond the Infinity Cache).
+__device__ __forceinline__ void nt_store16(uint4 *p, const uint4 &v) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<v4u *>(p));
+}
+
 // ABL (micro-benchmarks only, tools/ubench.py p1abl: the pass's cost by
 // stage): 0 the whole tile; 1 hash + bin and entry only; 2 + the rank
 // atomics; 3 + the scan and the run table; 4 + the scatter; 5 + the packing,
 // without the sorted tile's stores.  A stage's unconsumed results go to one
 // store that only an impossible value takes.
 template <int LAYOUT, bool SLOTS, bool COLS, int TB, int MK, int MAXB = 0, int MINW = 4,
-          int ABL = 0>
+          int ABL = 0, bool NT = false>
 __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                                                        uint64_t *__restrict__ pos_out,
                                                        uint32_t *__restrict__ runs, SegMap sm,
@@ -457,8 +464,18 @@ __global__ void __launch_bounds__(TB, MINW) k_part_bin(KeySpan ks, ModParams mp,
                               lshl_or(e[4], 21, e[3]), lshl_or(e[5], 10, e[4] >> 11));
         }
         if constexpr (ABL == 0) {
+            if constexpr (NT) {
+                // sorted tiles beyond the Infinity Cache (C5: 512 MiB): stored
+                // non-temporal, so they do not evict what pass 2 can use
+                // there (C5 build 0.419 -> 0.406 ms; below it, C2's 128 MiB,
+                // pass 2 reads them from the cache: 35 us, 48 from HBM; a
+                // runtime choice in the kernel spilled 3-4 VGPRs)
 #pragma unroll
-            for (int r = 0; r < kStores; r++) dst[r * TB + tid] = v[r];
+                for (int r = 0; r < kStores; r++) nt_store16(dst + r * TB + tid, v[r]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < kStores; r++) dst[r * TB + tid] = v[r];
+            }
         } else {
             // keep the packing: a store only when an impossible value shows
 #pragma unroll
@@ -777,6 +794,8 @@ __global__ void __launch_bounds__(kSuperBlock, 4) k_part_bin2(KeySpan ks, ModPar
 #pragma unroll
                     for (int z = 0; z < 6; z++) e[z] &= kEntryMask;
                 }
+                // (plain stores: non-temporal ones, as k_part_bin's at C5, made
+                // C4's pass 1 slower, 1.299 -> 1.317 ms, more than pass 2 gained)
                 dst[ph * kVecs + r * TB + tid] =
                     make_uint4(lshl_or(e[1], 21, e[0]), lshl_or(e[2], 10, e[1] >> 11),
                                lshl_or(e[4], 21, e[3]), lshl_or(e[5], 10, e[4] >> 11));
@@ -2068,6 +2087,19 @@ void bin_launch(const KeySpan &ks, const ModParams &mp, const PartitionWorkspace
     constexpr int kMinW = kWgs * TB / 256;  // waves per SIMD the registers must allow
     const size_t g = (size_t)device_cu_count() * kWgs;
     const unsigned grid = (unsigned)(ws.ntiles < g ? ws.ntiles : g);
+    if constexpr (!SLOTS && TB >= 1024 && MAXB == 1023) {
+        // builds whose sorted tiles exceed the Infinity Cache (C5): stored
+        // non-temporal (k_part_bin's NT)
+        if (ws.ntiles * (uint64_t)(TB * kPartKPT) * 8 > kInfinityCacheBytes) {
+            if (cols)
+                k_part_bin<L, SLOTS, true, TB, MK, MAXB, kMinW, 0, true><<<grid, TB, 0, stream>>>(
+                    ks, mp, ws.pos, runs, sm, ws.ntiles, slots);
+            else
+                k_part_bin<L, SLOTS, false, TB, MK, MAXB, kMinW, 0, true><<<grid, TB, 0, stream>>>(
+                    ks, mp, ws.pos, runs, sm, ws.ntiles, slots);
+            return;
+        }
+    }
     if (cols)
         k_part_bin<L, SLOTS, true, TB, MK, MAXB, kMinW><<<grid, TB, 0, stream>>>(
             ks, mp, ws.pos, runs, sm, ws.ntiles, slots);
