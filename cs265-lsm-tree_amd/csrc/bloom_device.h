@@ -1575,17 +1575,24 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
         const uint32_t vpb = 1u << (ls - 7);  // 16-B vectors per block
         const uint4 *seg4 = reinterpret_cast<const uint4 *>(seg);
         uint4 *w4 = reinterpret_cast<uint4 *>(words);
-        for (uint32_t q = tix; q < st.lad.d * vpb; q += BLOCK) {
+        auto block = [&](uint32_t q) -> uint4 * {
             uint32_t a = q >> (ls - 7);
             const uint32_t i = q & (vpb - 1u);
             if (st.lad.rinv) a = ladder0_block(a, (uint32_t)b, ls, st.lad.d, st.lad.rinv);
-            uint4 *dq = w4 + (((size_t)a << (lt - 7)) + ((size_t)b << (ls - 7)) + i);
-            uint4 v = seg4[q];
-            if (merge_existing) {
+            return w4 + (((size_t)a << (lt - 7)) + ((size_t)b << (ls - 7)) + i);
+        };
+        // (two loops: one loop with both stores under a branch had its
+        // stores merged into one plain store; the segments' note below)
+        if (merge_existing) {
+            for (uint32_t q = tix; q < st.lad.d * vpb; q += BLOCK) {
+                uint4 *dq = block(q);
+                uint4 v = seg4[q];
                 const uint4 o = *dq;
                 v.x |= o.x; v.y |= o.y; v.z |= o.z; v.w |= o.w;
+                *dq = v;
             }
-            *dq = v;
+        } else {
+            for (uint32_t q = tix; q < st.lad.d * vpb; q += BLOCK) nt_store16(block(q), seg4[q]);
         }
         return;
     }
@@ -1594,13 +1601,21 @@ __global__ void __launch_bounds__(BLOCK) k_part_apply(
     if (nseg == (int)seg_words) {  // seg_words % 4 == 0 and w0 is 16-B aligned
         uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
         const uint4 *seg4 = reinterpret_cast<const uint4 *>(seg);
-        for (int q = tix; q < (int)seg_words / 4; q += BLOCK) {
-            uint4 v = seg4[q];
-            if (merge_existing) {
+        if (merge_existing) {
+            for (int q = tix; q < (int)seg_words / 4; q += BLOCK) {
+                uint4 v = seg4[q];
                 const uint4 o = dst4[q];
                 v.x |= o.x; v.y |= o.y; v.z |= o.z; v.w |= o.w;
+                dst4[q] = v;
             }
-            dst4[q] = v;
+        } else {
+            // a fresh filter's finished segment: stored non-temporal, for
+            // later probes, not this build (the L2 and Infinity Cache keep the
+            // keys and sorted tiles: C2 188.6 -> 191.3, C4 129.1 -> 130.3
+            // Gkeys/s in the bench A/B); a merge stores plainly what it has
+            // just read (re-reading a non-temporal bitmap in repeated merges
+            // cost C2 0.0909 -> 0.0917 ms)
+            for (int q = tix; q < (int)seg_words / 4; q += BLOCK) nt_store16(dst4 + q, seg4[q]);
         }
     } else {
         for (int i = tix; i < nseg; i += BLOCK) {
