@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of one partition build (set_batch on device-resident keys)
+"""Interleaved A/B of one partition build (clear + set_batch on device-resident
+keys, the bench's step; before round 6's last change the children built
+without the clear, i.e. timed merge builds)
 between two builds of libbloomhip, in child processes on one GPU: A =
 cs265-lsm-tree_amd/lib_alt (tools/build_alt.sh REV), B = lib/.  Workloads:
 c2 (16.8M keys, m = 5 << 25), f10 (16.8M keys, m = 512,000,000), c5 (67M keys,
@@ -27,7 +29,8 @@ dk = torch.from_numpy(keys).cuda()
 f = bh.BloomFilter(m)
 f.set_strategy(bh.BUILD_PARTITION)
 s = torch.cuda.current_stream()
-def one():
+def one():  # the bench's step: a fresh filter (clear) and one build
+    f.clear(stream=s)
     f.set_batch(dk, stream=s)
 t0 = time.perf_counter()
 while time.perf_counter() - t0 < 0.5:
