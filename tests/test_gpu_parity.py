@@ -575,6 +575,23 @@ def test_c4_full_bitmap(golden):
     assert unpack_bools(got, keys[::97].size).all()
 
 
+@pytest.mark.parametrize("m", [5 << 23, 3 << 24, 41_943_053])
+def test_partition_merge_then_clear_rebuild(coracle, m):
+    """The partition build's two writebacks: a second batch ORs into the
+    first (merge: plain stores of the words it read) and, after clear(), a
+    fresh build writes every word of the bitmap (non-temporal stores, no
+    memset before it), on plan_build's ladder (d | 255) and on segments."""
+    a, b, c = rand_keys(400_000, 31), rand_keys(300_000, 32), rand_keys(500_000, 33)
+    f = bh.BloomFilter(m)
+    f.set_strategy(bh.BUILD_PARTITION)
+    f.set_batch(a)
+    f.set_batch(b)
+    assert (f.words() == coracle.build(m, np.concatenate([a, b]))).all()
+    f.clear()
+    f.set_batch(c)
+    assert (f.words() == coracle.build(m, c)).all()
+
+
 @pytest.mark.parametrize("m", [671_088_640, 360_000_007])
 def test_hbm_resident_pass2_ragged(coracle, m):
     """Builds whose sorted entries exceed the Infinity Cache (> 256 MiB, more
